@@ -1,0 +1,156 @@
+/*
+ * trajmpc.h -- C ABI of libtrajmpc.so, the MI355X (gfx950) batched MPC step.
+ *
+ * Drop-in boundary for the reference's hot path, DorianaG01/trajectory_generation
+ * MPC/mpc_6stati.py.  The reference exposes plain Python functions (no FFI); every
+ * entry point below is the batched, device-resident form of one of them, and the
+ * Python module trajectory_generation_amd/mpc_6stati.py binds these symbols with
+ * ctypes behind the reference's own signatures (INTEGRATION.md shows the binding).
+ *
+ *   reference (file:line)                      entry point here
+ *   mpc_6stati.py:9-19    Params               traj_vehicle_params / traj_default_params
+ *   mpc_6stati.py:25-53   tire_forces          traj_tire_forces_batch
+ *   mpc_6stati.py:55-71   f_cont               traj_f_cont_batch
+ *   mpc_6stati.py:73-97   numerical_jacobian   traj_numerical_jacobian_batch
+ *   mpc_6stati.py:99-109  linearize_discretize traj_linearize_discretize_batch
+ *   mpc_6stati.py:111-117 lateral_error        traj_lateral_error_batch
+ *   mpc_6stati.py:120-143 mpc_step kwargs      traj_mpc_config / traj_default_config
+ *   mpc_6stati.py:120-275 mpc_step             traj_mpc_step_batch (rollout, FD linearization,
+ *                                              condensed QP, ADMM + polish, status, info)
+ *   mpc_6stati.py:180-275 QP half only         traj_mpc_qp_batch (caller supplies A_k, B_k, g_k)
+ *   MPC/main.py:51-68     ref_window_from_x... traj_ref_window_batch
+ *   MPC/main.py:85-101    closed-loop loop     traj_closed_loop_step (window + mpc_step + plant)
+ *
+ * Conventions
+ *   - All array pointers are DEVICE pointers (hipMalloc / torch.cuda memory), row-major, float64
+ *     (the reference computes in numpy float64).  Shapes are given per argument.
+ *   - `stream` is a hipStream_t (NULL = default stream).  Calls are asynchronous; they never
+ *     allocate, copy to the host or synchronize, so they can be captured in a hipGraph.
+ *   - Return value: 0 on success, negative TRAJ_E_* on argument / launch errors.
+ *   - Per-instance solver outcome is written to `status` (TRAJ_STATUS_*, same numbering as the
+ *     CVXPY status strings listed below).  Like mpc_6stati.py:257-262, an instance whose status
+ *     is not OPTIMAL / OPTIMAL_INACCURATE gets u_cmd = u_prev and NaN in X_opt / U_opt / objective.
+ *   - Ownership: the caller owns every buffer.  The library holds no global state.
+ *   - Thread safety: reentrant; use one stream per host thread.
+ */
+#ifndef TRAJMPC_H
+#define TRAJMPC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRAJMPC_ABI_VERSION 1
+
+/* error codes (return values) */
+#define TRAJ_OK 0
+#define TRAJ_E_ARG (-1)          /* bad argument (null pointer, B < 0, N out of range, ...) */
+#define TRAJ_E_UNSUPPORTED (-2)  /* configuration this build does not implement */
+#define TRAJ_E_LAUNCH (-3)       /* HIP launch failure */
+
+/* per-instance status codes: CVXPY strings in brackets (mpc_6stati.py:257-262) */
+#define TRAJ_STATUS_OPTIMAL 0                /* "optimal" */
+#define TRAJ_STATUS_OPTIMAL_INACCURATE 1     /* "optimal_inaccurate" */
+#define TRAJ_STATUS_USER_LIMIT 2             /* "user_limit" (OSQP max_iter reached) */
+#define TRAJ_STATUS_INFEASIBLE 3             /* "infeasible" */
+#define TRAJ_STATUS_INFEASIBLE_INACCURATE 4  /* "infeasible_inaccurate" */
+#define TRAJ_STATUS_UNBOUNDED 5              /* "unbounded" */
+#define TRAJ_STATUS_SOLVER_ERROR 6           /* "Solver Error: SolverError" (non-finite data, ...) */
+
+/* mpc_6stati.py:9-19 (g is carried for layout parity; unused by the model, as in the reference) */
+typedef struct {
+    double Cm1, Cm2, Cr0, Cr2, Br, Cr, Dr, Bf, Cf, Df, m, Iz, lf, lr, g, maxAlpha, vx_zero;
+} traj_vehicle_params;
+
+/* mpc_step keyword arguments (mpc_6stati.py:120-143) + QP solver settings.  Solver defaults are
+ * CVXPY's OSQP settings (eps_abs = eps_rel = 1e-5, max_iter = 10000, polish on). */
+typedef struct {
+    int N;                            /* horizon, 1 <= N <= TRAJ_MAX_N */
+    double Ts;                        /* sampling time */
+    double q_c, q_phi, q_vx;          /* :128-131 */
+    double R[4], Rd[4];               /* :132-133, 2x2 row-major; the symmetric part is used */
+    double u_lo[2], u_hi[2];          /* u_bounds  :135-136 */
+    double du_lo[2], du_hi[2];        /* du_bounds :137-138 */
+    int has_x_lo, has_x_hi;           /* x_lo / x_hi given (:139-140, :208-213) */
+    double x_lo[6], x_hi[6];
+    double eps_abs, eps_rel, eps_prim_inf, rho, sigma, alpha, delta;
+    int max_iter, check_interval, scaling_iters, polish, polish_refine_iter, adaptive_rho;
+    double adaptive_rho_tol;
+    int polish_mode;                  /* 0: OSQP polish; 1: exact polish (KKT-certified optimum) */
+    int polish_max_pass;
+    double cert_tol;
+    int polish_max_rounds;
+} traj_mpc_config;
+
+#define TRAJ_MAX_N 40
+
+int traj_abi_version(void);
+const char* traj_status_string(int status);
+const char* traj_error_string(int err);
+
+/* defaults: mpc_6stati.py:9-19 and the mpc_step defaults (:120-143) with horizon N and step Ts */
+int traj_default_params(traj_vehicle_params* p);
+int traj_default_config(traj_mpc_config* c, int N, double Ts);
+
+/* ---- physics (mpc_6stati.py:25-117), B independent points ---- */
+int traj_tire_forces_batch(const traj_vehicle_params* p, int B, const double* x /*[B,6]*/,
+                           const double* u /*[B,2]*/, double* out /*[B,3] Fy_f, Fy_r, Frx*/, void* stream);
+int traj_f_cont_batch(const traj_vehicle_params* p, int B, const double* x /*[B,6]*/, const double* u /*[B,2]*/,
+                      double* xdot /*[B,6]*/, void* stream);
+int traj_numerical_jacobian_batch(const traj_vehicle_params* p, int B, const double* x /*[B,6]*/,
+                                  const double* u /*[B,2]*/, double eps_x, double eps_u, double* Jx /*[B,6,6]*/,
+                                  double* Ju /*[B,6,2]*/, double* f /*[B,6]*/, void* stream);
+int traj_linearize_discretize_batch(const traj_vehicle_params* p, int B, double Ts, const double* xbar /*[B,6]*/,
+                                    const double* ubar /*[B,2]*/, double* Ad /*[B,6,6]*/, double* Bd /*[B,6,2]*/,
+                                    double* g /*[B,6]*/, void* stream);
+int traj_lateral_error_batch(int B, const double* X, const double* Y, const double* Xref, const double* Yref,
+                             const double* phiref, double* out /*[B]*/, void* stream);
+
+/* ---- the MPC step (mpc_6stati.py:120-275) for B independent instances ----
+ * x0 [B,6], u_prev [B,2], path_ref [B,N+1,3], vref [B,N+1]  (vref None / scalar is expanded by the
+ * caller, :155-160).  Outputs: u_cmd [B,2], status [B]; optional (may be NULL): objective [B],
+ * X_opt [B,6,N+1], U_opt [B,2,N], iters [B] (ADMM iterations), polished [B] (1 if polish accepted). */
+int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
+                        const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
+                        int* status, double* objective, double* X_opt, double* U_opt, int* iters, int* polished,
+                        void* stream);
+
+/* QP half only (mpc_6stati.py:180-275) with the linearization supplied by the caller:
+ * Ad [B,N,6,6], Bd [B,N,6,2], g [B,N,6].  Same outputs as traj_mpc_step_batch. */
+int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
+                      const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
+                      const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
+                      double* X_opt, double* U_opt, int* iters, int* polished, void* stream);
+
+/* ---- closed loop (MPC/main.py) ----
+ * Reference path per trajectory (build-defined geometry): kind[b] = 0 cubic polynomial
+ * y = c0 + c1 x + c2 x^2 + c3 x^3 (parabola, main.py:64-66), 1 sinusoid y = c0 sin(c1 x + c2) + c3
+ * (MPC/README.md:73-76), 2 natural cubic spline through nk[b] knots xk[b,:] with piece coefficients
+ * coef[b,j,0..3] (linear extrapolation outside the knots).  pc [B,4]; xk [B,KMAX]; coef [B,KMAX-1,4]. */
+typedef struct {
+    int kmax;                 /* knot capacity per trajectory (>= 2 if any kind 2 path) */
+    const int* kind;          /* [B] */
+    const double* pc;         /* [B,4] */
+    const int* nk;            /* [B] (kind 2) */
+    const double* xk;         /* [B,kmax] */
+    const double* coef;       /* [B,kmax-1,4] */
+} traj_paths;
+
+/* main.py:51-68: window from x_start [B] with vref [B,N+1] -> path_ref [B,N+1,3] (phi* = atan(dy/dx)) */
+int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, const double* x_start,
+                          const double* vref, double* path_ref, void* stream);
+
+/* One closed-loop step of main.py:85-101 for B trajectories, in place:
+ *   path_ref = window(x[:,0]); u_cmd = mpc_step(x, u_prev, path_ref, vref); x += Ts f_cont(x, u_cmd);
+ *   u_prev = u_cmd.   x [B,6], u_prev [B,2] are updated; vref [B,N+1].
+ * If hist_x / hist_u are non-NULL the new state / command are also written to
+ * hist_x[b, t+1, :] ([B,T+1,6]) and hist_u[b, t, :] ([B,T,2]) with T = hist_T.
+ * status / iters [B] (optional) receive this step's solver outcome. */
+int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
+                          double* x, double* u_prev, const double* vref, int t, int hist_T, double* hist_x,
+                          double* hist_u, int* status, int* iters, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

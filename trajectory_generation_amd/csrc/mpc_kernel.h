@@ -1,0 +1,882 @@
+// mpc_kernel.h -- the fused batched MPC step for gfx950: one workgroup per trajectory instance.
+//
+// Reference hot path: MPC/mpc_6stati.py:120-275 (mpc_step).  Per instance the kernel runs
+//   1. nominal rollout          :165-172  x_{k+1} = x_k + Ts f(x_k, u_prev)
+//   2. linearize/discretize     :175-178  central differences (:73-97), A = I + Ts Jx, B = Ts Ju,
+//                                          g = x + Ts f - A x - B u (:99-109)
+//   3. the TV-LQ QP             :180-250  condensed over U (X eliminated by the dynamics)
+//   4. the solve                :252-262  OSQP's ADMM (Ruiz scaling, sigma/alpha, adaptive rho,
+//                                          OSQP termination) + polish, as restated in oracle/
+//   5. status / info            :257-275  u_cmd = U[:,0] or u_prev; X_opt by the linear model
+//
+// Layout (DESIGN.md "Kernel"): thread i (< n = 2N) owns QP variable i = 2k + channel, its box row
+// and its rate row.  Matrices live ROW-PER-LANE in registers: the KKT matrix
+// K = P + sigma I + A' diag(rho) A is inverted in place by the symmetric sweep operator
+// (n pivots, each a broadcast of one column through LDS), so every ADMM iteration is one dense
+// register mat-vec (n FMAs/lane) plus two +-2 neighbour exchanges for the banded constraint rows.
+// The scaled cost matrix P (needed for residuals, rho updates and polish) stays in LDS.
+// Everything is float64, like the reference.
+#pragma once
+#include "physics.h"
+
+namespace tgmpc {
+
+constexpr double INFTY = 1e30;
+constexpr double DIV_TOL = 1e-30;
+constexpr double MIN_SCALING = 1e-4;
+constexpr double MAX_SCALING = 1e4;
+constexpr double RHO_MIN = 1e-6;
+constexpr double RHO_MAX = 1e6;
+constexpr double RHO_TOL = 1e-4;
+constexpr double RHO_EQ_OVER_INEQ = 1e3;
+
+struct PathArgs {
+    int kmax;
+    const int* kind;
+    const double* pc;
+    const int* nk;
+    const double* xk;
+    const double* coef;
+};
+
+struct KArgs {
+    traj_vehicle_params p;
+    traj_mpc_config c;
+    int B;
+    const double* x0;        // [B,6]  (closed loop: state, updated in place)
+    const double* u_prev;    // [B,2]
+    const double* path_ref;  // [B,N+1,3] (unused in closed loop)
+    const double* vref;      // [B,N+1]
+    const double* Ad;        // [B,N,6,6] (QP-only mode)
+    const double* Bd;
+    const double* gd;
+    double* u_cmd;           // [B,2]
+    int* status;
+    double* objective;
+    double* X_opt;           // [B,6,N+1]
+    double* U_opt;           // [B,2,N]
+    int* iters;
+    int* polished;
+    // closed loop
+    PathArgs path;
+    double* x_state;         // [B,6]
+    double* u_state;         // [B,2]
+    int t, hist_T;
+    double* hist_x;          // [B,T+1,6]
+    double* hist_u;          // [B,T,2]
+};
+
+__device__ __forceinline__ double limit_scaling(double v) {
+    return v < MIN_SCALING ? 1.0 : (v > MAX_SCALING ? MAX_SCALING : v);
+}
+
+// reference path y(x), dy/dx for the closed-loop window (DESIGN.md "reference paths")
+__device__ inline void path_eval(const PathArgs& pa, int b, double x, double& y, double& dy) {
+    int kind = pa.kind[b];
+    const double* c = pa.pc + 4 * b;
+    if (kind == 0) {
+        y = c[0] + x * (c[1] + x * (c[2] + x * c[3]));
+        dy = c[1] + x * (2.0 * c[2] + x * 3.0 * c[3]);
+    } else if (kind == 1) {
+        double a = c[1] * x + c[2];
+        double s, co;
+        sincos(a, &s, &co);
+        y = c[0] * s + c[3];
+        dy = c[0] * c[1] * co;
+    } else {
+        int nk = pa.nk[b];
+        const double* xk = pa.xk + (size_t)pa.kmax * b;
+        const double* cf = pa.coef + (size_t)(pa.kmax - 1) * 4 * b;
+        if (x <= xk[0]) {
+            y = cf[0] + cf[1] * (x - xk[0]);
+            dy = cf[1];
+        } else if (x >= xk[nk - 1]) {
+            const double* q = cf + 4 * (nk - 2);
+            double h = xk[nk - 1] - xk[nk - 2];
+            double ye = q[0] + h * (q[1] + h * (q[2] + h * q[3]));
+            double se = q[1] + h * (2.0 * q[2] + h * 3.0 * q[3]);
+            y = ye + se * (x - xk[nk - 1]);
+            dy = se;
+        } else {
+            int j = 0;
+            while (j < nk - 2 && x >= xk[j + 1]) ++j;
+            const double* q = cf + 4 * j;
+            double tt = x - xk[j];
+            y = q[0] + tt * (q[1] + tt * (q[2] + tt * q[3]));
+            dy = q[1] + tt * (2.0 * q[2] + tt * 3.0 * q[3]);
+        }
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void wave_max(double (&v)[V]) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            double o = __shfl_xor(v[i], off, 64);
+            v[i] = (o > v[i] || o != o) ? o : v[i];
+        }
+    }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// =====================================================================================
+// The kernel.  NN = capacity in QP variables (>= 2N), LIN = compute the linearization (else read
+// Ad/Bd/g), CLOSED = closed-loop step (window from the state, plant update, history).
+// =====================================================================================
+template <int NN, bool LIN, bool CLOSED>
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const KArgs a) {
+    constexpr int WAVES = (NN + 63) / 64;
+    constexpr int NT = WAVES * 64;
+    constexpr int NM = NN / 2;          // max horizon
+    constexpr int PS = NN + 1;          // padded row stride of P in LDS
+    constexpr int NFD = 12;             // FD perturbations per stage (vars 2..5 and u, +/-)
+    constexpr int BIG = (NM * NFD * 6 > NN * PS) ? NM * NFD * 6 : NN * PS;
+
+    __shared__ double s_pref[3 * (NM + 1)];
+    __shared__ double s_vref[NM + 1];
+    __shared__ double s_x0[6], s_up[2];
+    __shared__ double s_xbar[(NM + 1) * 6];
+    __shared__ double s_fbar[NM * 6];
+    __shared__ double s_A[NM * 36];
+    __shared__ double s_B[NM * 12];
+    __shared__ double s_g[NM * 6];
+    __shared__ double s_big[BIG];       // FD outputs, then the scaled P (row stride PS)
+    __shared__ double s_xh[(NM + 1) * 6];
+    __shared__ double s_sc[(NM + 1) * 2];
+    __shared__ double s_e[(NM + 1) * 3];
+    __shared__ double s_ex[6 * NN];     // exchange / broadcast buffers (rotating)
+    __shared__ double s_red[16 * WAVES];
+    __shared__ int s_flag[4];
+
+    const traj_vehicle_params& p = a.p;
+    const traj_mpc_config& c = a.c;
+    const int b = blockIdx.x;
+    const int t = threadIdx.x;
+    const int lane = t & 63, wid = t >> 6;
+    const int N = c.N, n = 2 * N;
+    const double Ts = c.Ts;
+    const bool own = t < n;             // owns variable / rows t
+    const int kk = t >> 1, ch = t & 1;  // stage and channel of variable t
+    int xb = 0;                         // rotating exchange buffer
+
+    // ---- block helpers -------------------------------------------------------------
+    auto exch = [&](double v, int delta) -> double {   // value of variable t+delta (0 outside)
+        double* buf = s_ex + (xb & 3) * NN;
+        xb++;
+        if (own) buf[t] = v;
+        __syncthreads();
+        int s = t + delta;
+        return (own && s >= 0 && s < n) ? buf[s] : 0.0;
+    };
+    auto bcast = [&](double v) -> double* {            // publish v_t for all, returns buffer
+        double* buf = s_ex + (xb & 3) * NN;
+        xb++;
+        if (own) buf[t] = v;
+        __syncthreads();
+        return buf;
+    };
+    auto block_max = [&](auto& v) {                   // in-place max over the block
+        constexpr int V = sizeof(v) / sizeof(double);
+        wave_max<V>(v);
+        if (WAVES > 1) {
+            if (lane == 0)
+                for (int i = 0; i < V; ++i) s_red[wid * V + i] = v[i];
+            __syncthreads();
+            for (int i = 0; i < V; ++i) {
+                double m = s_red[i];
+                for (int w = 1; w < WAVES; ++w) m = fmax(m, s_red[w * V + i]);
+                v[i] = m;
+            }
+            __syncthreads();
+        }
+    };
+    auto block_sum = [&](double v) -> double {
+        v = wave_sum(v);
+        if (WAVES > 1) {
+            if (lane == 0) s_red[wid] = v;
+            __syncthreads();
+            double s = 0.0;
+            for (int w = 0; w < WAVES; ++w) s += s_red[w];
+            __syncthreads();
+            v = s;
+        }
+        return v;
+    };
+
+    // ---- 0. inputs -----------------------------------------------------------------
+    if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+    if (CLOSED) {
+        if (t < 6) s_x0[t] = a.x_state[6 * b + t];
+        if (t < 2) s_up[t] = a.u_state[2 * b + t];
+    } else {
+        if (t < 6) s_x0[t] = a.x0[6 * b + t];
+        if (t < 2) s_up[t] = a.u_prev[2 * b + t];
+    }
+    for (int i = t; i < N + 1; i += NT) s_vref[i] = a.vref[(size_t)(N + 1) * b + i];
+    if (!CLOSED)
+        for (int i = t; i < 3 * (N + 1); i += NT) s_pref[i] = a.path_ref[(size_t)3 * (N + 1) * b + i];
+    __syncthreads();
+    if (CLOSED) {
+        // MPC/main.py:51-68: xs_0 = X, xs_{k+1} = xs_k + vref_k Ts; ys = path(xs); phi* = atan(path'(xs))
+        if (t == 0) {
+            double xs = s_x0[0];
+            s_pref[0] = xs;
+            for (int k = 0; k < N; ++k) {
+                xs = xs + s_vref[k] * Ts;
+                s_pref[3 * (k + 1)] = xs;
+            }
+        }
+        __syncthreads();
+        for (int k = t; k <= N; k += NT) {
+            double y, dy;
+            path_eval(a.path, b, s_pref[3 * k], y, dy);
+            s_pref[3 * k + 1] = y;
+            s_pref[3 * k + 2] = atan(dy);
+        }
+        __syncthreads();
+    }
+    {
+        int bad = 0;
+        for (int i = t; i < 3 * (N + 1); i += NT) bad |= !isfinite(s_pref[i]);
+        for (int i = t; i < N + 1; i += NT) bad |= !isfinite(s_vref[i]);
+        if (t < 6) bad |= !isfinite(s_x0[t]);
+        if (t < 2) bad |= !isfinite(s_up[t]);
+        if (bad) s_flag[0] = 1;
+    }
+
+    // ---- 1. nominal rollout (:165-172) ---------------------------------------------
+    if (t == 0) {
+        double x[6], f[6], sd, cd;
+        sincos(s_up[1], &sd, &cd);
+        for (int i = 0; i < 6; ++i) { x[i] = s_x0[i]; s_xbar[i] = x[i]; }
+        for (int k = 0; k < N; ++k) {
+            f_cont_sc(p, x, s_up[0], s_up[1], sd, cd, f);
+            for (int i = 0; i < 6; ++i) {
+                s_fbar[6 * k + i] = f[i];
+                x[i] = x[i] + Ts * f[i];
+                s_xbar[6 * (k + 1) + i] = x[i];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- 2. linearization (:175-178 -> :73-109) ------------------------------------
+    if (LIN) {
+        const double eps = 1e-5;
+        for (int it = t; it < NFD * N; it += NT) {
+            int k = it / NFD, q = it % NFD;
+            double x[6], u[2], f[6];
+            for (int i = 0; i < 6; ++i) x[i] = s_xbar[6 * k + i];
+            u[0] = s_up[0];
+            u[1] = s_up[1];
+            double dd = (q & 1) ? -eps : eps;
+            // x + dx / x - dx with dx = eps e_j  (x_i + 0.0 elsewhere, as numpy does)
+            if (q < 8) {
+                int v = 2 + (q >> 1);
+                for (int i = 0; i < 6; ++i) x[i] = (q & 1) ? x[i] - (i == v ? eps : 0.0) : x[i] + (i == v ? eps : 0.0);
+                (void)dd;
+            } else {
+                int v = (q - 8) >> 1;
+                for (int i = 0; i < 2; ++i) u[i] = (q & 1) ? u[i] - (i == v ? eps : 0.0) : u[i] + (i == v ? eps : 0.0);
+            }
+            f_cont(p, x, u, f);
+            for (int i = 0; i < 6; ++i) s_big[(k * NFD + q) * 6 + i] = f[i];
+        }
+        __syncthreads();
+        // Jx columns 0,1 are exactly zero (f does not read X, Y: f(x+dx) - f(x-dx) == 0 bit for bit)
+        for (int it = t; it < 8 * N; it += NT) {
+            int k = it >> 3, col = it & 7;
+            for (int r = 0; r < 6; ++r) {
+                double J = 0.0;
+                if (col >= 2) {
+                    int q = (col - 2) * 2;   // perturbation index of (+) for this column (state 2..5, u 0..1)
+                    J = (s_big[(k * NFD + q) * 6 + r] - s_big[(k * NFD + q + 1) * 6 + r]) / (2.0 * eps);
+                }
+                if (col < 6) s_A[k * 36 + r * 6 + col] = ((r == col) ? 1.0 : 0.0) + Ts * J;
+                else s_B[k * 12 + r * 2 + (col - 6)] = Ts * J;
+            }
+        }
+        __syncthreads();
+        for (int it = t; it < 6 * N; it += NT) {
+            int k = it / 6, r = it % 6;
+            double ax = 0.0, bu = 0.0;
+            for (int cc = 0; cc < 6; ++cc) ax += s_A[k * 36 + r * 6 + cc] * s_xbar[6 * k + cc];
+            for (int cc = 0; cc < 2; ++cc) bu += s_B[k * 12 + r * 2 + cc] * s_up[cc];
+            s_g[6 * k + r] = s_xbar[6 * k + r] + Ts * s_fbar[6 * k + r] - ax - bu;
+        }
+    } else {
+        const size_t o = (size_t)b * N;
+        for (int i = t; i < 36 * N; i += NT) s_A[i] = a.Ad[o * 36 + i];
+        for (int i = t; i < 12 * N; i += NT) s_B[i] = a.Bd[o * 12 + i];
+        for (int i = t; i < 6 * N; i += NT) s_g[i] = a.gd[o * 6 + i];
+    }
+    __syncthreads();
+
+    // ---- 3. condensed QP (:180-250) --------------------------------------------------
+    // free response xh_{k+1} = A_k xh_k + g_k
+    if (t < 6) s_xh[t] = s_x0[t];
+    __syncthreads();
+    for (int k = 0; k < N; ++k) {
+        if (t < 6) {
+            double v = 0.0;
+            for (int cc = 0; cc < 6; ++cc) v += s_A[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
+            s_xh[6 * (k + 1) + t] = v + s_g[6 * k + t];
+        }
+        __syncthreads();
+    }
+    // per stage: sin/cos(phi*), tracking errors e_k of the free response, constant cost
+    const double W0 = c.q_c, W1 = c.q_phi, W2 = c.q_vx;
+    for (int k = t; k <= N; k += NT) {
+        double Pr = s_pref[3 * k + 2], s, co;
+        sincos(Pr, &s, &co);
+        s_sc[2 * k] = s;
+        s_sc[2 * k + 1] = co;
+        const double* xk = s_xh + 6 * k;
+        double e0 = s * (xk[0] - s_pref[3 * k]) - co * (xk[1] - s_pref[3 * k + 1]);
+        double e1 = xk[2] - Pr;
+        double e2 = xk[3] - s_vref[k];
+        s_e[3 * k] = e0;
+        s_e[3 * k + 1] = e1;
+        s_e[3 * k + 2] = e2;
+    }
+    __syncthreads();
+
+    double Prow[NN];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) Prow[j] = 0.0;
+    double qi = 0.0;
+    {
+        // sensitivity column j = t of G_k (6-vector), propagated forward; P accumulated row-wise
+        double G[6] = {0, 0, 0, 0, 0, 0};
+        for (int k = 0; k < N; ++k) {
+            if (own) {
+                if (t < 2 * k) {
+                    double Gn[6];
+                    for (int r = 0; r < 6; ++r) {
+                        double v = 0.0;
+                        for (int cc = 0; cc < 6; ++cc) v = fma(s_A[k * 36 + r * 6 + cc], G[cc], v);
+                        Gn[r] = v;
+                    }
+                    for (int r = 0; r < 6; ++r) G[r] = Gn[r];
+                } else if (kk == k) {
+                    for (int r = 0; r < 6; ++r) G[r] = s_B[k * 12 + r * 2 + ch];
+                }
+            }
+            // output sensitivities of stage k+1: F = C_{k+1} G
+            const double s = s_sc[2 * (k + 1)], co = s_sc[2 * (k + 1) + 1];
+            double F0 = s * G[0] - co * G[1], F1 = G[2], F2 = G[3];
+            double* buf = s_ex + (xb & 1) * 3 * NN;   // 2 rotating slots of 3*NN
+            xb++;
+            if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
+            __syncthreads();
+            if (own) {
+                double w0 = 2.0 * W0 * F0, w1 = 2.0 * W1 * F1, w2 = 2.0 * W2 * F2;
+                const double* ek = s_e + 3 * (k + 1);
+                qi += w0 * ek[0] + w1 * ek[1] + w2 * ek[2];
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+                    if (j < n) Prow[j] = fma(w0, buf[j], fma(w1, buf[NN + j], fma(w2, buf[2 * NN + j], Prow[j])));
+            }
+        }
+        __syncthreads();
+    }
+    // input penalties U'RU and dU'Rd dU (dU_0 = U_0 - u_prev)
+    double Rs[4], Rds[4];
+    Rs[0] = c.R[0]; Rs[3] = c.R[3]; Rs[1] = Rs[2] = 0.5 * (c.R[1] + c.R[2]);
+    Rds[0] = c.Rd[0]; Rds[3] = c.Rd[3]; Rds[1] = Rds[2] = 0.5 * (c.Rd[1] + c.Rd[2]);
+    // this thread's rows of Rs / Rds (selects, not a dynamic index: keeps them in registers)
+    const double Rs0 = ch ? Rs[2] : Rs[0], Rs1 = ch ? Rs[3] : Rs[1];
+    const double Rd0 = ch ? Rds[2] : Rds[0], Rd1 = ch ? Rds[3] : Rds[1];
+    if (own) {
+        const double dmul = (kk < N - 1) ? 2.0 : 1.0;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            if (j < n) {
+                int kj = j >> 1;
+                double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
+                double add = 0.0;
+                if (kj == kk) add = 2.0 * rs + 2.0 * rd * dmul;
+                else if (kj == kk - 1 || kj == kk + 1) add = -2.0 * rd;
+                Prow[j] += add;
+            }
+        }
+        if (kk == 0) qi -= 2.0 * (Rd0 * s_up[0] + Rd1 * s_up[1]);
+    }
+
+    // constraint rows owned by t: box (U_t) and rate (U_t - U_{t-2}, or U_0 - u_prev)
+    double lb = ch ? c.u_lo[1] : c.u_lo[0], ub = ch ? c.u_hi[1] : c.u_hi[0];
+    double lr = ch ? c.du_lo[1] : c.du_lo[0], ur = ch ? c.du_hi[1] : c.du_hi[0];
+    if (kk == 0) { lr += s_up[ch]; ur += s_up[ch]; }
+    const bool has_prev = kk > 0;  // rate row couples t-2
+    // non-finite data -> solver error
+    {
+        int bad = 0;
+        if (own) {
+            bad |= !isfinite(qi);
+#pragma unroll
+            for (int j = 0; j < NN; ++j)
+                if (j < n) bad |= !isfinite(Prow[j]);
+        }
+        if (bad) s_flag[0] = 1;
+    }
+    // exact feasibility of the box+rate chain (interval propagation); decides INFEASIBLE up front
+    if (t < 2) {
+        double lo = s_up[t], hi = s_up[t];
+        const double dlo = t ? c.du_lo[1] : c.du_lo[0], dhi = t ? c.du_hi[1] : c.du_hi[0];
+        const double ulo = t ? c.u_lo[1] : c.u_lo[0], uhi = t ? c.u_hi[1] : c.u_hi[0];
+        for (int k = 0; k < N; ++k) {
+            double nlo = lo + dlo, nhi = hi + dhi;
+            if (nlo < ulo) nlo = ulo;
+            if (nhi > uhi) nhi = uhi;
+            if (!(nlo <= nhi)) { s_flag[1] = 1; }
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    __syncthreads();
+    const int early = s_flag[0] ? TRAJ_STATUS_SOLVER_ERROR : (s_flag[1] ? TRAJ_STATUS_INFEASIBLE : -1);
+
+    int status = TRAJ_STATUS_SOLVER_ERROR, iter = 0, pol = 0;
+    double xsol = 0.0;  // unscaled U_t at exit
+
+    if (early < 0) {
+        // ---- 4a. Ruiz equilibration + cost scaling (OSQP scale_data) ---------------
+        double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0;
+        for (int it = 0; it < c.scaling_iters; ++it) {
+            double Er_up = exch(Er, +2);     // E of rate row t+2
+            double D_dn = exch(D, -2);       // D of variable t-2
+            double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
+            double pn = 0.0;
+#pragma unroll
+            for (int j = 0; j < NN; ++j)
+                if (j < n) pn = fmax(pn, fabs(Prow[j]));
+            double coln = fmax(pn, fmax(fabs(a_b), fmax(fabs(a_r), fabs(a_rp))));
+            double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
+            double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
+            double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
+            double* Dv = bcast(Dt);
+            if (own) {
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+                    if (j < n) Prow[j] *= Dt * Dv[j];
+            }
+            qi *= Dt;
+            D *= Dt;
+            Eb *= Etb;
+            Er *= Etr;
+            // cost scaling
+            double cn = 0.0;
+#pragma unroll
+            for (int j = 0; j < NN; ++j)
+                if (j < n) cn = fmax(cn, fabs(Prow[j]));
+            double mean = block_sum(own ? cn : 0.0) / n;
+            double qv[1] = {own ? fabs(qi) : 0.0};
+            block_max(qv);
+            double ct = fmax(mean, limit_scaling(qv[0]));
+            ct = 1.0 / limit_scaling(ct);
+            if (own) {
+#pragma unroll
+                for (int j = 0; j < NN; ++j) Prow[j] *= ct;
+            }
+            qi *= ct;
+            cs *= ct;
+        }
+        const double Dinv = 1.0 / D, Ebinv = 1.0 / Eb, Erinv = 1.0 / Er, csinv = 1.0 / cs;
+        const double D_dn = exch(D, -2), Er_up = exch(Er, +2);
+        const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
+        // scaled bounds
+        double slb = (lb > -INFTY) ? lb * Eb : -INFTY, sub = (ub < INFTY) ? ub * Eb : INFTY;
+        double slr = (lr > -INFTY) ? lr * Er : -INFTY, sur = (ur < INFTY) ? ur * Er : INFTY;
+        // scaled P to LDS (row stride PS)
+        if (own) {
+#pragma unroll
+            for (int j = 0; j < NN; ++j)
+                if (j < n) s_big[t * PS + j] = Prow[j];
+        }
+        __syncthreads();
+
+        // ---- helpers over the scaled problem ----------------------------------------
+        // A x (box, rate) for the vector v owned row-wise
+        auto Ax = [&](double v, double& zb, double& zr) {
+            double vdn = exch(v, -2);
+            zb = a_b * v;
+            zr = a_r * v - a_rm * vdn;
+        };
+        // A' w for w = (wb, wr)
+        auto ATw = [&](double wb, double wr) -> double {
+            double wr_up = exch(wr, +2);
+            return a_b * wb + a_r * wr - a_rp * wr_up;
+        };
+        auto Pmul = [&](double v) -> double {  // (P v)_t
+            double* vb = bcast(v);
+            double s = 0.0;
+            if (own) {
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+                    if (j < n) s = fma(s_big[t * PS + j], vb[j], s);
+            }
+            return s;
+        };
+        double Krow[NN];
+        auto Kmul = [&](double v) -> double {
+            double* vb = bcast(v);
+            double s = 0.0;
+            if (own) {
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+                    if (j < n) s = fma(Krow[j], vb[j], s);
+            }
+            return s;
+        };
+        auto rho_for = [&](double l, double u, double rho) -> double {
+            if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
+            if (u - l < RHO_TOL) return RHO_EQ_OVER_INEQ * rho;
+            return rho;
+        };
+        // residuals (OSQP update_info, unscaled) : out[0..6] unscaled, [7..13] scaled norms
+        struct Res { double pr, dr, eps_p, eps_d, prs, drs, axs, zs, pxs, atys, qs; };
+        auto residuals = [&](double x, double zb, double zr, double yb, double yr) -> Res {
+            double axb, axr;
+            Ax(x, axb, axr);
+            double px = Pmul(x);
+            double aty = ATw(yb, yr);
+            double v[13];
+            if (own) {
+                double dres = px + qi + aty;
+                v[0] = fmax(fabs(Ebinv * (axb - zb)), fabs(Erinv * (axr - zr)));   // prim res
+                v[1] = fmax(fabs(Ebinv * axb), fabs(Erinv * axr));
+                v[2] = fmax(fabs(Ebinv * zb), fabs(Erinv * zr));
+                v[3] = fabs(Dinv * dres) * csinv;
+                v[4] = fabs(Dinv * px) * csinv;
+                v[5] = fabs(Dinv * aty) * csinv;
+                v[6] = fabs(Dinv * qi) * csinv;
+                v[7] = fmax(fabs(axb - zb), fabs(axr - zr));
+                v[8] = fabs(dres);
+                v[9] = fmax(fabs(axb), fabs(axr));
+                v[10] = fmax(fabs(zb), fabs(zr));
+                v[11] = fabs(px);
+                v[12] = fmax(fabs(aty), fabs(qi));
+            } else {
+                for (int i = 0; i < 13; ++i) v[i] = 0.0;
+            }
+            double atys_only = own ? fabs(aty) : 0.0, qs_only = own ? fabs(qi) : 0.0;
+            block_max(v);
+            double w2[2] = {atys_only, qs_only};
+            block_max(w2);
+            Res r;
+            r.pr = v[0];
+            r.eps_p = c.eps_abs + c.eps_rel * fmax(v[1], v[2]);
+            r.dr = v[3];
+            r.eps_d = c.eps_abs + c.eps_rel * fmax(v[4], fmax(v[5], v[6]));
+            r.prs = v[7]; r.drs = v[8]; r.axs = v[9]; r.zs = v[10]; r.pxs = v[11];
+            r.atys = w2[0]; r.qs = w2[1];
+            return r;
+        };
+
+        // ---- 4b/4c. ADMM (OSQP osqp_solve) + polish (polish.c) --------------------------
+        // A state machine around ONE factorization site (so the register-resident inverse is
+        // never handed to an out-of-line call): each pass of the outer loop builds
+        //   K = P + ks I + A' diag(kb, kr) A
+        // (ADMM: kb/kr = rho, ks = sigma; polish: kb/kr = active/delta, ks = delta) and inverts it
+        // in place with the symmetric sweep operator, then runs the phase until it needs a new K.
+        constexpr int PH_ADMM = 0, PH_POLISH = 1, PH_DONE = 2;
+        int phase = PH_ADMM;
+        double rho = c.rho;
+        double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
+        double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
+        Res r = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        int rounds = 0, ps = 0, actb = 0, actr = 0;
+        double escale = 1.0;
+        const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
+        const double a_r_up = exch(a_r, +2);
+        iter = 1;
+        while (phase != PH_DONE) {
+            // ---- build K (row t) ----
+            const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
+            const double kr = (phase == PH_ADMM) ? rr : (actr ? 1.0 / dl : 0.0);
+            const double ks = (phase == PH_ADMM) ? sig : dl;
+            {
+                const double kr_up = exch(kr, +2);
+                const double dii = ks + kb * a_b * a_b + kr * a_r * a_r + kr_up * a_rp * a_rp;
+                const double dm = -kr * a_r * a_rm;        // (t, t-2)
+                const double dp = -kr_up * a_r_up * a_rp;  // (t, t+2)
+#pragma unroll
+                for (int j = 0; j < NN; ++j) {
+                    double v;
+                    if (own) {
+                        v = (j < n) ? s_big[t * PS + j] : 0.0;
+                        v += (j == t) ? dii : 0.0;
+                        v += (j == t - 2) ? dm : 0.0;
+                        v += (j == t + 2) ? dp : 0.0;
+                    } else {
+                        v = (j == t) ? 1.0 : 0.0;   // identity padding for rows n..NN-1
+                    }
+                    Krow[j] = v;
+                }
+            }
+            // ---- sweep: Krow <- row t of K^{-1} (NN pivots, fully unrolled; padding pivots are 1) ----
+            bool ok = true;
+#pragma unroll
+            for (int pv = 0; pv < NN; ++pv) {
+                double* cb = s_ex + (4 + (pv & 1)) * NN;
+                if (t < NN) cb[t] = Krow[pv];
+                __syncthreads();
+                const double d = cb[pv];
+                ok = ok && (d > 0.0);
+                const double dinv = 1.0 / d;
+                if (t == pv) {
+#pragma unroll
+                    for (int j = 0; j < NN; ++j)
+                        if (j != pv) Krow[j] = cb[j] * dinv;
+                    Krow[pv] = -dinv;
+                } else {
+                    const double fd = Krow[pv] * dinv;
+#pragma unroll
+                    for (int j = 0; j < NN; ++j)
+                        if (j != pv) Krow[j] = fma(-fd, cb[j], Krow[j]);
+                    Krow[pv] = fd;
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < NN; ++j) Krow[j] = -Krow[j];
+            if (!ok) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
+
+            if (phase == PH_ADMM) {
+                bool converged = false, refactor = false;
+                for (; iter <= c.max_iter; ++iter) {
+                    // rhs = sig x - q + A'(rho z - y)
+                    double rhs = sig * x - qi + ATw(rb * zb - yb, rr * zr - yr);
+                    double xt = Kmul(rhs);
+                    double ztb, ztr;
+                    Ax(xt, ztb, ztr);
+                    double xn = alpha * xt + (1.0 - alpha) * x;
+                    double zrb = alpha * ztb + (1.0 - alpha) * zb;
+                    double zrr = alpha * ztr + (1.0 - alpha) * zr;
+                    double vb = zrb + yb / rb, vr = zrr + yr / rr;
+                    double nzb = clampd(vb, slb, sub), nzr = clampd(vr, slr, sur);
+                    yb = yb + rb * (zrb - nzb);
+                    yr = yr + rr * (zrr - nzr);
+                    x = xn;
+                    zb = nzb;
+                    zr = nzr;
+                    if (iter % c.check_interval == 0) {
+                        r = residuals(x, zb, zr, yb, yr);
+                        if (r.pr <= escale * r.eps_p && r.dr <= escale * r.eps_d) { converged = true; break; }
+                        if (c.adaptive_rho) {
+                            double pn = fmax(r.axs, r.zs);
+                            double dn = fmax(r.pxs, fmax(r.atys, r.qs));
+                            double est = rho * sqrt((r.prs / (pn + DIV_TOL)) / (r.drs / (dn + DIV_TOL) + DIV_TOL));
+                            est = fmin(fmax(est, RHO_MIN), RHO_MAX);
+                            if (est > rho * c.adaptive_rho_tol || est < rho / c.adaptive_rho_tol) {
+                                rho = est;
+                                rb = rho_for(slb, sub, rho);
+                                rr = rho_for(slr, sur, rho);
+                                refactor = true;
+                                ++iter;
+                                break;
+                            }
+                        }
+                    }
+                }
+                if (refactor && iter <= c.max_iter) continue;
+                if (converged) status = TRAJ_STATUS_OPTIMAL;
+                else {
+                    iter = c.max_iter;
+                    r = residuals(x, zb, zr, yb, yr);
+                    status = (r.pr <= 10.0 * r.eps_p && r.dr <= 10.0 * r.eps_d) ? TRAJ_STATUS_OPTIMAL_INACCURATE
+                                                                                  : TRAJ_STATUS_USER_LIMIT;
+                }
+                if (status == TRAJ_STATUS_OPTIMAL && c.polish) {
+                    // OSQP active sets: lower if z - l < -y, upper if u - z < y
+                    actb = own ? ((zb - slb < -yb) ? -1 : ((sub - zb < yb) ? 1 : 0)) : 0;
+                    actr = own ? ((zr - slr < -yr) ? -1 : ((sur - zr < yr) ? 1 : 0)) : 0;
+                    ps = 1;
+                    phase = PH_POLISH;
+                } else {
+                    phase = PH_DONE;
+                }
+                continue;
+            }
+
+            // ---- PH_POLISH: Krow = row of M^{-1}, M = P + dI + Ar'Ar/d (eliminated reduced KKT) ----
+            {
+                const double bb = actb < 0 ? slb : (actb > 0 ? sub : 0.0);
+                const double br = actr < 0 ? slr : (actr > 0 ? sur : 0.0);
+                double px_ = 0.0, pyb = 0.0, pyr = 0.0;
+                double r1 = -qi, r2b = actb ? bb : 0.0, r2r = actr ? br : 0.0;
+                double axb = 0.0, axr = 0.0;
+                for (int rf = 0; rf <= c.polish_refine_iter; ++rf) {
+                    double tv = Kmul(r1 + ATw(actb ? r2b / dl : 0.0, actr ? r2r / dl : 0.0));
+                    double tb, tr;
+                    Ax(tv, tb, tr);
+                    px_ += tv;
+                    if (actb) pyb += (tb - r2b) / dl;
+                    if (actr) pyr += (tr - r2r) / dl;
+                    if (rf == c.polish_refine_iter) break;
+                    double Pxv = Pmul(px_);
+                    double atyv = ATw(pyb, pyr);
+                    r1 = -qi - Pxv - atyv;
+                    Ax(px_, axb, axr);
+                    r2b = actb ? bb - axb : 0.0;
+                    r2r = actr ? br - axr : 0.0;
+                }
+                Ax(px_, axb, axr);
+                if (c.polish_mode == 0) {
+                    // z = proj(Ax + y), y = Ax + y - z (OSQP project_normalcone); accept if residuals drop
+                    double ztb = axb + pyb, ztr = axr + pyr;
+                    double nzb = clampd(ztb, slb, sub), nzr = clampd(ztr, slr, sur);
+                    double nyb = ztb - nzb, nyr = ztr - nzr;
+                    Res rp = residuals(px_, nzb, nzr, nyb, nyr);
+                    bool okp = (rp.pr < r.pr && rp.dr < r.dr) || (rp.pr < r.pr && r.dr < 1e-10) ||
+                               (rp.dr < r.dr && r.pr < 1e-10);
+                    if (okp) {
+                        x = px_; zb = nzb; zr = nzr; yb = nyb; yr = nyr;
+                        pol = 1;
+                    }
+                    phase = PH_DONE;
+                    continue;
+                }
+                // exact mode: KKT certificate in the unscaled problem
+                double Pxv = Pmul(px_);
+                double atyv = ATw(pyb, pyr);
+                const double tol = c.cert_tol;
+                double v[2];
+                v[0] = own ? fabs(Dinv * (Pxv + qi + atyv)) * csinv : 0.0;            // stationarity
+                v[1] = own ? fmax(fabs(Dinv * qi), fabs(Dinv * Pxv)) * csinv : 0.0;  // gradient scale
+                block_max(v);
+                double gsc = fmax(1.0, v[1]);
+                int okc = v[0] <= tol * gsc;
+                if (own) {
+                    double axu = axb * Ebinv, arv = axr * Erinv;
+                    if (slb > -INFTY && axu < lb - tol * (1.0 + fabs(lb))) okc = 0;
+                    if (sub < INFTY && axu > ub + tol * (1.0 + fabs(ub))) okc = 0;
+                    if (slr > -INFTY && arv < lr - tol * (1.0 + fabs(lr))) okc = 0;
+                    if (sur < INFTY && arv > ur + tol * (1.0 + fabs(ur))) okc = 0;
+                    double ybu = pyb * Eb * csinv, yru = pyr * Er * csinv;
+                    if (actb < 0 && ybu > tol * gsc) okc = 0;
+                    if (actb > 0 && ybu < -tol * gsc) okc = 0;
+                    if (actr < 0 && yru > tol * gsc) okc = 0;
+                    if (actr > 0 && yru < -tol * gsc) okc = 0;
+                }
+                double fo[1] = {okc ? 0.0 : 1.0};
+                block_max(fo);
+                if (fo[0] == 0.0) {
+                    x = px_;
+                    zb = clampd(axb, slb, sub);
+                    zr = clampd(axr, slr, sur);
+                    yb = pyb;
+                    yr = pyr;
+                    pol = ps + 16 * rounds;
+                    phase = PH_DONE;
+                    continue;
+                }
+                if (ps < c.polish_max_pass) {
+                    // primal-dual active-set update with the OSQP rule on the polished (Ax, y)
+                    actb = own ? ((axb - slb < -pyb) ? -1 : ((sub - axb < pyb) ? 1 : 0)) : 0;
+                    actr = own ? ((axr - slr < -pyr) ? -1 : ((sur - axr < pyr) ? 1 : 0)) : 0;
+                    ++ps;
+                    continue;
+                }
+                if (rounds < c.polish_max_rounds && iter < c.max_iter) {
+                    // not certified: continue ADMM to a 100x tighter tolerance, then polish again
+                    ++rounds;
+                    escale *= 1e-2;
+                    ++iter;
+                    phase = PH_ADMM;
+                    continue;
+                }
+                phase = PH_DONE;
+            }
+        }
+        if (iter > c.max_iter) iter = c.max_iter;
+        xsol = D * x;
+    } else {
+        status = early;
+        iter = 0;
+    }
+
+    // ---- 5. outputs (:257-275) ------------------------------------------------------
+    const bool good = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
+    double* Ubuf = s_ex;  // U (stage-major) for the X rollout
+    __syncthreads();
+    if (own) Ubuf[t] = xsol;
+    __syncthreads();
+    // X_opt by the linear model X_{k+1} = A_k X_k + B_k U_k + g_k (s_xh reused)
+    if (t < 6) s_xh[t] = s_x0[t];
+    __syncthreads();
+    for (int k = 0; k < N; ++k) {
+        if (t < 6) {
+            double v = 0.0;
+            for (int cc = 0; cc < 6; ++cc) v += s_A[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
+            v += s_B[k * 12 + t * 2] * Ubuf[2 * k] + s_B[k * 12 + t * 2 + 1] * Ubuf[2 * k + 1] + s_g[6 * k + t];
+            s_xh[6 * (k + 1) + t] = v;
+        }
+        __syncthreads();
+    }
+    // objective = cost of :217-250 at (X_opt, U_opt)
+    double op = 0.0;
+    for (int k = t; k <= N; k += NT) {
+        const double* X = s_xh + 6 * k;
+        double s = s_sc[2 * k], co = s_sc[2 * k + 1];
+        double ec = s * (X[0] - s_pref[3 * k]) - co * (X[1] - s_pref[3 * k + 1]);
+        double ep = X[2] - s_pref[3 * k + 2];
+        double ev = X[3] - s_vref[k];
+        op += c.q_c * ec * ec + c.q_phi * ep * ep + c.q_vx * ev * ev;
+        if (k < N) {
+            double u0 = Ubuf[2 * k], u1 = Ubuf[2 * k + 1];
+            double d0 = u0 - (k == 0 ? s_up[0] : Ubuf[2 * k - 2]);
+            double d1 = u1 - (k == 0 ? s_up[1] : Ubuf[2 * k - 1]);
+            op += u0 * (c.R[0] * u0 + c.R[1] * u1) + u1 * (c.R[2] * u0 + c.R[3] * u1);
+            op += d0 * (c.Rd[0] * d0 + c.Rd[1] * d1) + d1 * (c.Rd[2] * d0 + c.Rd[3] * d1);
+        }
+    }
+    double obj = block_sum(op);
+    const double nan = __builtin_nan("");
+    double uc0 = good ? Ubuf[0] : s_up[0], uc1 = good ? Ubuf[1] : s_up[1];
+    if (CLOSED) {
+        // plant x <- x + Ts f(x, u_cmd) (main.py:97), u_prev <- u_cmd (:101)
+        if (t == 0) {
+            double xs[6], f[6], u[2] = {uc0, uc1};
+            for (int i = 0; i < 6; ++i) xs[i] = s_x0[i];
+            f_cont(p, xs, u, f);
+            for (int i = 0; i < 6; ++i) {
+                double xn = xs[i] + Ts * f[i];
+                a.x_state[6 * b + i] = xn;
+                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + a.t + 1) * 6 + i] = xn;
+            }
+            a.u_state[2 * b] = uc0;
+            a.u_state[2 * b + 1] = uc1;
+            if (a.hist_u) {
+                a.hist_u[((size_t)b * a.hist_T + a.t) * 2] = uc0;
+                a.hist_u[((size_t)b * a.hist_T + a.t) * 2 + 1] = uc1;
+            }
+            if (a.status) a.status[b] = status;
+            if (a.iters) a.iters[b] = iter;
+        }
+        return;
+    }
+    if (t == 0) {
+        a.u_cmd[2 * b] = uc0;
+        a.u_cmd[2 * b + 1] = uc1;
+        a.status[b] = status;
+        if (a.objective) a.objective[b] = good ? obj : nan;
+        if (a.iters) a.iters[b] = iter;
+        if (a.polished) a.polished[b] = pol;
+    }
+    if (a.U_opt && own) a.U_opt[(size_t)b * 2 * N + ch * N + kk] = good ? xsol : nan;
+    if (a.X_opt) {
+        for (int i = t; i < 6 * (N + 1); i += NT) {
+            int r = i / (N + 1), k = i % (N + 1);
+            a.X_opt[(size_t)b * 6 * (N + 1) + i] = good ? s_xh[6 * k + r] : nan;
+        }
+    }
+}
+
+}  // namespace tgmpc

@@ -1,0 +1,343 @@
+// trajmpc.hip -- C ABI of libtrajmpc.so (declared in include/trajmpc.h).
+//
+// Batched physics kernels (one thread per point) and the dispatch of the fused MPC kernel
+// (mpc_kernel.h) by horizon capacity.  Built for gfx950 only:
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -shared -fPIC
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../include/trajmpc.h"
+#include "mpc_kernel.h"
+#include "physics.h"
+
+namespace tgmpc {
+
+// ---------------------------------------------------------------- physics kernels
+
+__global__ void tire_forces_kernel(traj_vehicle_params p, int B, const double* x, const double* u, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    double Fyf, Fyr, Frx;
+    tire_forces(p, x[6 * i + 3], x[6 * i + 4], x[6 * i + 5], u[2 * i], u[2 * i + 1], Fyf, Fyr, Frx);
+    out[3 * i] = Fyf;
+    out[3 * i + 1] = Fyr;
+    out[3 * i + 2] = Frx;
+}
+
+__global__ void f_cont_kernel(traj_vehicle_params p, int B, const double* x, const double* u, double* xd) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    double xs[6], us[2], f[6];
+    for (int j = 0; j < 6; ++j) xs[j] = x[6 * i + j];
+    us[0] = u[2 * i];
+    us[1] = u[2 * i + 1];
+    f_cont(p, xs, us, f);
+    for (int j = 0; j < 6; ++j) xd[6 * i + j] = f[j];
+}
+
+// mpc_6stati.py:73-97 (all 16 central differences + f, like the reference)
+__device__ void numjac(const traj_vehicle_params& p, const double* x, const double* u, double ex, double eu,
+                       double* Jx, double* Ju, double* f) {
+    double xp[6], xm[6], up[2], um[2], fp[6], fm[6];
+    for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 6; ++j) {
+            double dx = (j == i) ? ex : 0.0;
+            xp[j] = x[j] + dx;
+            xm[j] = x[j] - dx;
+        }
+        f_cont(p, xp, u, fp);
+        f_cont(p, xm, u, fm);
+        for (int r = 0; r < 6; ++r) Jx[r * 6 + i] = (fp[r] - fm[r]) / (2.0 * ex);
+    }
+    for (int i = 0; i < 2; ++i) {
+        for (int j = 0; j < 2; ++j) {
+            double du = (j == i) ? eu : 0.0;
+            up[j] = u[j] + du;
+            um[j] = u[j] - du;
+        }
+        f_cont(p, x, up, fp);
+        f_cont(p, x, um, fm);
+        for (int r = 0; r < 6; ++r) Ju[r * 2 + i] = (fp[r] - fm[r]) / (2.0 * eu);
+    }
+    f_cont(p, x, u, f);
+}
+
+__global__ void numjac_kernel(traj_vehicle_params p, int B, const double* x, const double* u, double ex, double eu,
+                              double* Jx, double* Ju, double* f) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    double xs[6], us[2], jx[36], ju[12], fv[6];
+    for (int j = 0; j < 6; ++j) xs[j] = x[6 * i + j];
+    us[0] = u[2 * i];
+    us[1] = u[2 * i + 1];
+    numjac(p, xs, us, ex, eu, jx, ju, fv);
+    for (int j = 0; j < 36; ++j) Jx[36 * i + j] = jx[j];
+    for (int j = 0; j < 12; ++j) Ju[12 * i + j] = ju[j];
+    for (int j = 0; j < 6; ++j) f[6 * i + j] = fv[j];
+}
+
+// mpc_6stati.py:99-109
+__global__ void lindisc_kernel(traj_vehicle_params p, int B, double Ts, const double* x, const double* u, double* Ad,
+                               double* Bd, double* g) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    double xs[6], us[2], jx[36], ju[12], fv[6], A[36], Bm[12];
+    for (int j = 0; j < 6; ++j) xs[j] = x[6 * i + j];
+    us[0] = u[2 * i];
+    us[1] = u[2 * i + 1];
+    numjac(p, xs, us, 1e-5, 1e-5, jx, ju, fv);
+    for (int r = 0; r < 6; ++r)
+        for (int cc = 0; cc < 6; ++cc) A[r * 6 + cc] = ((r == cc) ? 1.0 : 0.0) + Ts * jx[r * 6 + cc];
+    for (int j = 0; j < 12; ++j) Bm[j] = Ts * ju[j];
+    for (int r = 0; r < 6; ++r) {
+        double ax = 0.0, bu = 0.0;
+        for (int cc = 0; cc < 6; ++cc) ax += A[r * 6 + cc] * xs[cc];
+        for (int cc = 0; cc < 2; ++cc) bu += Bm[r * 2 + cc] * us[cc];
+        g[6 * i + r] = xs[r] + Ts * fv[r] - ax - bu;
+    }
+    for (int j = 0; j < 36; ++j) Ad[36 * i + j] = A[j];
+    for (int j = 0; j < 12; ++j) Bd[12 * i + j] = Bm[j];
+}
+
+__global__ void lateral_error_kernel(int B, const double* X, const double* Y, const double* Xr, const double* Yr,
+                                     const double* Pr, double* out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    out[i] = lateral_error(X[i], Y[i], Xr[i], Yr[i], Pr[i]);
+}
+
+// main.py:51-68 batched (one thread per trajectory: the x-advance is a running sum)
+__global__ void ref_window_kernel(PathArgs pa, int B, int N, double Ts, const double* x_start, const double* vref,
+                                  double* pref) {
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double xs = x_start[b];
+    for (int k = 0; k <= N; ++k) {
+        if (k > 0) xs = xs + vref[(size_t)(N + 1) * b + k - 1] * Ts;
+        double y, dy;
+        path_eval(pa, b, xs, y, dy);
+        double* o = pref + ((size_t)(N + 1) * b + k) * 3;
+        o[0] = xs;
+        o[1] = y;
+        o[2] = atan(dy);
+    }
+}
+
+// ---------------------------------------------------------------- MPC dispatch
+
+// per-capacity launchers (mpc_inst.hip compiled once per NN)
+#define TGMPC_CAPACITIES(X) X(16) X(32) X(40) X(64) X(80)
+#define TGMPC_DECL(NNV) int launch_mpc_##NNV(const KArgs& a, hipStream_t st, int mode);
+TGMPC_CAPACITIES(TGMPC_DECL)
+#undef TGMPC_DECL
+
+static int launch_mpc(const KArgs& a, hipStream_t st, int mode) {
+    const int n = 2 * a.c.N;
+#define TGMPC_CASE(NNV) \
+    if (n <= NNV) return launch_mpc_##NNV(a, st, mode);
+    TGMPC_CAPACITIES(TGMPC_CASE)
+#undef TGMPC_CASE
+    return TRAJ_E_ARG;
+}
+
+static int check_cfg(const traj_mpc_config* c) {
+    if (!c) return TRAJ_E_ARG;
+    if (c->N < 1 || c->N > TRAJ_MAX_N) return TRAJ_E_ARG;
+    if (!(c->Ts > 0.0) || c->max_iter < 1 || c->check_interval < 1 || c->scaling_iters < 0) return TRAJ_E_ARG;
+    if (c->polish_mode != 0 && c->polish_mode != 1) return TRAJ_E_ARG;
+    if (c->has_x_lo || c->has_x_hi) {
+        // state bounds (mpc_6stati.py:208-213): accepted only when every bound is infinite
+        for (int i = 0; i < 6; ++i) {
+            if (c->has_x_lo && c->x_lo[i] > -INFTY) return TRAJ_E_UNSUPPORTED;
+            if (c->has_x_hi && c->x_hi[i] < INFTY) return TRAJ_E_UNSUPPORTED;
+        }
+    }
+    return TRAJ_OK;
+}
+
+static inline unsigned nblk(int B, int bs) { return (unsigned)((B + bs - 1) / bs); }
+
+}  // namespace tgmpc
+
+using namespace tgmpc;
+
+extern "C" {
+
+int traj_abi_version(void) { return TRAJMPC_ABI_VERSION; }
+
+const char* traj_status_string(int s) {
+    switch (s) {
+        case TRAJ_STATUS_OPTIMAL: return "optimal";
+        case TRAJ_STATUS_OPTIMAL_INACCURATE: return "optimal_inaccurate";
+        case TRAJ_STATUS_USER_LIMIT: return "user_limit";
+        case TRAJ_STATUS_INFEASIBLE: return "infeasible";
+        case TRAJ_STATUS_INFEASIBLE_INACCURATE: return "infeasible_inaccurate";
+        case TRAJ_STATUS_UNBOUNDED: return "unbounded";
+        case TRAJ_STATUS_SOLVER_ERROR: return "Solver Error: SolverError";
+        default: return "unknown";
+    }
+}
+
+const char* traj_error_string(int e) {
+    switch (e) {
+        case TRAJ_OK: return "ok";
+        case TRAJ_E_ARG: return "invalid argument";
+        case TRAJ_E_UNSUPPORTED: return "unsupported configuration";
+        case TRAJ_E_LAUNCH: return "HIP launch failure";
+        default: return "unknown error";
+    }
+}
+
+int traj_default_params(traj_vehicle_params* p) {
+    if (!p) return TRAJ_E_ARG;
+    p->Cm1 = 0.287; p->Cm2 = 0.0545; p->Cr0 = 0.0518; p->Cr2 = 0.00035;
+    p->Br = 3.3852; p->Cr = 1.2691; p->Dr = 0.1737;
+    p->Bf = 2.579; p->Cf = 1.2; p->Df = 0.192;
+    p->m = 0.041; p->Iz = 27.8e-6; p->lf = 0.029; p->lr = 0.033;
+    p->g = 9.81; p->maxAlpha = 0.6; p->vx_zero = 0.3;
+    return TRAJ_OK;
+}
+
+int traj_default_config(traj_mpc_config* c, int N, double Ts) {
+    if (!c) return TRAJ_E_ARG;
+    std::memset(c, 0, sizeof(*c));
+    c->N = N; c->Ts = Ts;
+    c->q_c = 6.0; c->q_phi = 0.5; c->q_vx = 0.5;
+    c->R[0] = 0.02; c->R[3] = 2.0;
+    c->Rd[0] = 0.01; c->Rd[3] = 5.0;
+    c->u_lo[0] = -1.0; c->u_hi[0] = 1.0; c->u_lo[1] = -0.6; c->u_hi[1] = 0.6;
+    c->du_lo[0] = -0.5; c->du_hi[0] = 0.5; c->du_lo[1] = -0.3; c->du_hi[1] = 0.3;
+    c->eps_abs = 1e-5; c->eps_rel = 1e-5; c->eps_prim_inf = 1e-4;
+    c->rho = 0.1; c->sigma = 1e-6; c->alpha = 1.6; c->delta = 1e-6;
+    c->max_iter = 10000; c->check_interval = 25; c->scaling_iters = 10;
+    c->polish = 1; c->polish_refine_iter = 3; c->adaptive_rho = 1; c->adaptive_rho_tol = 5.0;
+    c->polish_mode = 0; c->polish_max_pass = 8; c->cert_tol = 1e-9; c->polish_max_rounds = 2;
+    return TRAJ_OK;
+}
+
+int traj_tire_forces_batch(const traj_vehicle_params* p, int B, const double* x, const double* u, double* out,
+                           void* stream) {
+    if (!p || B < 0 || (B > 0 && (!x || !u || !out))) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    hipLaunchKernelGGL(tire_forces_kernel, dim3(nblk(B, 256)), dim3(256), 0, (hipStream_t)stream, *p, B, x, u, out);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_f_cont_batch(const traj_vehicle_params* p, int B, const double* x, const double* u, double* xdot,
+                      void* stream) {
+    if (!p || B < 0 || (B > 0 && (!x || !u || !xdot))) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    hipLaunchKernelGGL(f_cont_kernel, dim3(nblk(B, 256)), dim3(256), 0, (hipStream_t)stream, *p, B, x, u, xdot);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_numerical_jacobian_batch(const traj_vehicle_params* p, int B, const double* x, const double* u,
+                                  double eps_x, double eps_u, double* Jx, double* Ju, double* f, void* stream) {
+    if (!p || B < 0 || (B > 0 && (!x || !u || !Jx || !Ju || !f))) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    hipLaunchKernelGGL(numjac_kernel, dim3(nblk(B, 128)), dim3(128), 0, (hipStream_t)stream, *p, B, x, u, eps_x,
+                       eps_u, Jx, Ju, f);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_linearize_discretize_batch(const traj_vehicle_params* p, int B, double Ts, const double* xbar,
+                                    const double* ubar, double* Ad, double* Bd, double* g, void* stream) {
+    if (!p || B < 0 || (B > 0 && (!xbar || !ubar || !Ad || !Bd || !g))) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    hipLaunchKernelGGL(lindisc_kernel, dim3(nblk(B, 128)), dim3(128), 0, (hipStream_t)stream, *p, B, Ts, xbar, ubar,
+                       Ad, Bd, g);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_lateral_error_batch(int B, const double* X, const double* Y, const double* Xref, const double* Yref,
+                             const double* phiref, double* out, void* stream) {
+    if (B < 0 || (B > 0 && (!X || !Y || !Xref || !Yref || !phiref || !out))) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    hipLaunchKernelGGL(lateral_error_kernel, dim3(nblk(B, 256)), dim3(256), 0, (hipStream_t)stream, B, X, Y, Xref,
+                       Yref, phiref, out);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
+                      const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
+                      const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
+                      double* X_opt, double* U_opt, int* iters, int* polished, void* stream, bool lin) {
+    if (!p || B < 0) return TRAJ_E_ARG;
+    int e = check_cfg(c);
+    if (e) return e;
+    if (B == 0) return TRAJ_OK;
+    if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
+    if (!lin && (!Ad || !Bd || !g)) return TRAJ_E_ARG;
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.p = *p;
+    a.c = *c;
+    a.B = B;
+    a.x0 = x0; a.u_prev = u_prev; a.path_ref = path_ref; a.vref = vref;
+    a.Ad = Ad; a.Bd = Bd; a.gd = g;
+    a.u_cmd = u_cmd; a.status = status; a.objective = objective; a.X_opt = X_opt; a.U_opt = U_opt;
+    a.iters = iters; a.polished = polished;
+    return launch_mpc(a, (hipStream_t)stream, lin ? 0 : 1);
+}
+
+int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
+                        const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
+                        int* status, double* objective, double* X_opt, double* U_opt, int* iters, int* polished,
+                        void* stream) {
+    return mpc_common(p, c, B, x0, u_prev, path_ref, vref, nullptr, nullptr, nullptr, u_cmd, status, objective,
+                      X_opt, U_opt, iters, polished, stream, true);
+}
+
+int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
+                      const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
+                      const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
+                      double* X_opt, double* U_opt, int* iters, int* polished, void* stream) {
+    return mpc_common(p, c, B, x0, u_prev, path_ref, vref, Ad, Bd, g, u_cmd, status, objective, X_opt, U_opt, iters,
+                      polished, stream, false);
+}
+
+static bool paths_ok(const traj_paths* ps) {
+    return ps && ps->kind && ps->pc && (ps->kmax < 2 || (ps->nk && ps->xk && ps->coef));
+}
+
+int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, const double* x_start,
+                          const double* vref, double* path_ref, void* stream) {
+    if (B < 0 || N < 1 || !paths_ok(paths)) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!x_start || !vref || !path_ref) return TRAJ_E_ARG;
+    PathArgs pa{paths->kmax, paths->kind, paths->pc, paths->nk, paths->xk, paths->coef};
+    hipLaunchKernelGGL(ref_window_kernel, dim3(nblk(B, 128)), dim3(128), 0, (hipStream_t)stream, pa, B, N, Ts,
+                       x_start, vref, path_ref);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
+                          double* x, double* u_prev, const double* vref, int t, int hist_T, double* hist_x,
+                          double* hist_u, int* status, int* iters, void* stream) {
+    if (!p || B < 0 || !paths_ok(paths)) return TRAJ_E_ARG;
+    int e = check_cfg(c);
+    if (e) return e;
+    if (B == 0) return TRAJ_OK;
+    if (!x || !u_prev || !vref) return TRAJ_E_ARG;
+    if ((hist_x || hist_u) && (t < 0 || t >= hist_T)) return TRAJ_E_ARG;
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.p = *p;
+    a.c = *c;
+    a.B = B;
+    a.vref = vref;
+    a.path = PathArgs{paths->kmax, paths->kind, paths->pc, paths->nk, paths->xk, paths->coef};
+    a.x_state = x;
+    a.u_state = u_prev;
+    a.t = t;
+    a.hist_T = hist_T;
+    a.hist_x = hist_x;
+    a.hist_u = hist_u;
+    a.status = status;
+    a.iters = iters;
+    return launch_mpc(a, (hipStream_t)stream, 2);
+}
+
+}  // extern "C"

@@ -1,0 +1,184 @@
+"""Drop-in replacement for the reference module MPC/mpc_6stati.py.
+
+Same public names, signatures, argument meaning, return values and error behaviour as the
+reference; every computation runs in the HIP kernels of libtrajmpc.so on the GPU.
+
+  Params                  mpc_6stati.py:9-19
+  clamp                   :21-23
+  tire_forces             :25-53
+  f_cont                  :55-71
+  numerical_jacobian      :73-97
+  linearize_discretize    :99-109
+  lateral_error           :111-117
+  mpc_step                :120-275  -> (u_cmd ndarray(2,), status str, info dict)
+
+`mpc_step` keeps the reference's contract:
+  * x0 / u_prev reshaped to (6,) / (2,) (numpy errors propagate); path_ref must be (N+1, 3)
+    (AssertionError otherwise, :151); vref None -> x0[3], scalar -> filled, else reshaped (N+1,).
+  * status in ("optimal", "optimal_inaccurate") -> (U[:,0], status, info) with info keys
+    status / objective / X_opt (6,N+1) / U_opt (2,N) / path_ref / vref  (:264-275).
+  * any other status -> (u_prev, status, {})  (:261-262); a solver failure ->
+    (u_prev, "Solver Error: <Exception>", {})  (:257-259).
+  * `solver` is accepted and ignored (the QP is solved by the HIP ADMM); `verbose` is ignored.
+The QP's optimum is unique (R > 0), so the result is the one OSQP returns when its polish
+succeeds; see DESIGN.md "Parity" for the stated tolerances.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import batch as _b
+from ._lib import STATUS_STRINGS
+
+# Vehicle Parameters (mpc_6stati.py:9-19)
+Params = dict(_b.REFERENCE_PARAMS)
+
+
+def clamp(x, lo, hi):
+    """Utility to constrain values within a range (mpc_6stati.py:21-23)."""
+    return np.minimum(np.maximum(x, lo), hi)
+
+
+def _np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy()
+
+
+def tire_forces(x, u, p):
+    """(Fy_f, Fy_r, Frx) at x (6,), u (2,) -- mpc_6stati.py:25-53 (HIP kernel)."""
+    out = _np(_b.tire_forces_batch(np.asarray(x, np.float64).reshape(1, 6), np.asarray(u, np.float64).reshape(1, 2),
+                                   p))[0]
+    return out[0], out[1], out[2]
+
+
+def f_cont(x, u, p):
+    """Continuous-time dynamics f(x,u) -> ndarray (6,) -- mpc_6stati.py:55-71 (HIP kernel)."""
+    return _np(_b.f_cont_batch(np.asarray(x, np.float64).reshape(1, 6), np.asarray(u, np.float64).reshape(1, 2),
+                               p))[0]
+
+
+def numerical_jacobian(f, x, u, p, eps_x=1e-5, eps_u=1e-5):
+    """Central-difference Jacobians (Jx, Ju, f(x,u)) -- mpc_6stati.py:73-97.
+
+    For the model's own f_cont the differences run in the HIP kernel; any other callable f is
+    differenced exactly as the reference does, calling f."""
+    x = np.asarray(x, np.float64)
+    u = np.asarray(u, np.float64)
+    if f is f_cont and x.size == 6 and u.size == 2:
+        Jx, Ju, fv = _b.numerical_jacobian_batch(x.reshape(1, 6), u.reshape(1, 2), p, eps_x, eps_u)
+        return _np(Jx)[0], _np(Ju)[0], _np(fv)[0]
+    n, m = x.size, u.size
+    Jx = np.zeros((n, n))
+    Ju = np.zeros((n, m))
+    for i in range(n):
+        dx = np.zeros(n); dx[i] = eps_x
+        Jx[:, i] = (f(x + dx, u, p) - f(x - dx, u, p)) / (2.0 * eps_x)
+    for j in range(m):
+        du = np.zeros(m); du[j] = eps_u
+        Ju[:, j] = (f(x, u + du, p) - f(x, u - du, p)) / (2.0 * eps_u)
+    return Jx, Ju, f(x, u, p)
+
+
+def linearize_discretize(x_bar, u_bar, Ts, p):
+    """(Ad, Bd, g) -- mpc_6stati.py:99-109 (HIP kernel)."""
+    A, B, g = _b.linearize_discretize_batch(np.asarray(x_bar, np.float64).reshape(1, 6),
+                                            np.asarray(u_bar, np.float64).reshape(1, 2), Ts, p)
+    return _np(A)[0], _np(B)[0], _np(g)[0]
+
+
+def lateral_error(X, Y, Xref, Yref, phiref):
+    """e_c = sin(phi_ref)(X - Xref) - cos(phi_ref)(Y - Yref) -- mpc_6stati.py:111-117 (HIP kernel)."""
+    args = [np.asarray(v, np.float64) for v in (X, Y, Xref, Yref, phiref)]
+    shape = np.broadcast(*args).shape
+    flat = [np.broadcast_to(a, shape).reshape(-1) for a in args]
+    out = _np(_b.lateral_error_batch(*flat)).reshape(shape)
+    return out[()] if shape == () else out
+
+
+def _is_psd(M):
+    S = 0.5 * (M + M.T)
+    w = np.linalg.eigvalsh(S)
+    return w.min() >= -1e-12 * max(1.0, np.abs(w).max())
+
+
+def mpc_step(
+    x0,
+    u_prev,
+    path_ref,
+    Ts=0.02,
+    N=20,
+    params=None,
+    q_c=6.0,
+    q_phi=0.5,
+    q_vx=0.5,
+    R=np.diag([0.02, 2.0]),
+    Rd=np.diag([0.01, 5.0]),
+    vref=None,
+    u_bounds=((-1.0, 1.0), (-0.6, 0.6)),
+    du_bounds=((-0.5, 0.5), (-0.3, 0.3)),
+    x_lo=None,
+    x_hi=None,
+    solver="OSQP",
+    verbose=False,
+    **solver_settings,
+):
+    """One MPC step (mpc_6stati.py:120-275); see the module docstring for the contract."""
+    p = dict(Params)
+    if params is not None:
+        p.update(params)
+    x0 = np.asarray(x0).reshape(6).astype(np.float64)
+    u_pr = np.asarray(u_prev).reshape(2).astype(np.float64)
+    path_ref = np.asarray(path_ref)
+    assert path_ref.shape[0] == N + 1 and path_ref.shape[1] == 3
+    if vref is None:
+        vref = np.full(N + 1, x0[3])
+    elif np.isscalar(vref):
+        vref = np.full(N + 1, float(vref))
+    else:
+        vref = np.asarray(vref).reshape(N + 1)
+    R = np.asarray(R, dtype=np.float64)
+    Rd = np.asarray(Rd, dtype=np.float64)
+    if not (_is_psd(R) and _is_psd(Rd)):
+        # cvxpy rejects a non-convex quad_form at prob.solve (inside the reference's try, :255-259)
+        return u_pr, "Solver Error: DCPError", {}
+    cfg = _b.config_struct(N=N, Ts=Ts, q_c=q_c, q_phi=q_phi, q_vx=q_vx, R=R, Rd=Rd, u_bounds=u_bounds,
+                           du_bounds=du_bounds, x_lo=x_lo, x_hi=x_hi, **solver_settings)
+    o = _b.mpc_step_batch(x0.reshape(1, 6), u_pr.reshape(1, 2), path_ref.astype(np.float64).reshape(1, N + 1, 3),
+                          vref.astype(np.float64).reshape(1, N + 1), cfg, p)
+    st = int(o["status"][0].item())
+    status = STATUS_STRINGS.get(st, "Solver Error: SolverError")
+    if st == 6:
+        return u_pr, status, {}
+    if status not in ("optimal", "optimal_inaccurate"):
+        return u_pr, status, {}
+    u_cmd = _np(o["u_cmd"])[0].reshape(2)
+    info = {
+        "status": status,
+        "objective": float(o["objective"][0].item()),
+        "X_opt": _np(o["X_opt"])[0],
+        "U_opt": _np(o["U_opt"])[0],
+        "path_ref": path_ref,
+        "vref": vref,
+    }
+    return u_cmd, status, info
+
+
+def mpc_step_batch(x0, u_prev, path_ref, vref=None, Ts=0.02, N=20, params=None, **kwargs):
+    """Batched mpc_step: x0 [B,6], u_prev [B,2], path_ref [B,N+1,3], vref [B,N+1] / [N+1] / scalar / None.
+    Returns a dict of torch.cuda tensors (see batch.mpc_step_batch)."""
+    x0 = torch.as_tensor(x0, dtype=torch.float64)
+    B = x0.reshape(-1, 6).shape[0]
+    if vref is None:
+        vref = x0.reshape(B, 6)[:, 3:4].expand(B, N + 1)
+    elif np.isscalar(vref):
+        vref = torch.full((B, N + 1), float(vref), dtype=torch.float64)
+    else:
+        vref = torch.as_tensor(vref, dtype=torch.float64)
+        if vref.dim() == 1:
+            vref = vref.reshape(1, N + 1).expand(B, N + 1)
+    solver_keys = {k: kwargs.pop(k) for k in list(kwargs) if k not in (
+        "q_c", "q_phi", "q_vx", "R", "Rd", "u_bounds", "du_bounds", "x_lo", "x_hi")}
+    solver_keys.pop("solver", None)
+    solver_keys.pop("verbose", None)
+    cfg = _b.config_struct(N=N, Ts=Ts, **kwargs, **solver_keys)
+    return _b.mpc_step_batch(x0, u_prev, path_ref, vref, cfg, params)
