@@ -1,0 +1,189 @@
+"""bench.py -- MPC steps/sec on B parallel spline-tracking trajectories (BASELINE.json configs[1]).
+
+One bench step = one closed-loop step of MPC/main.py:85-101 for all B trajectories of this rank
+(reference window -> mpc_step -> Euler plant), i.e. ONE launch of the fused HIP kernel
+(traj_closed_loop_step).  Inputs and state are resident in HBM for the whole timed region.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 20] [--dt 0.05]
+  N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
+
+Multi-GPU: trajectories are independent, so each rank owns its own B trajectories (ids
+rank*B .. rank*B+B-1, weak scaling) with no data-path collective; the ranks only meet at the
+timing barriers and the max-over-ranks reduction of the elapsed time.
+
+Prints ONE JSON line (rank 0) with the metric, the roofline of the dominant kernel and the CPU
+baseline (the C oracle -- a restatement of the reference path -- on a bounded sample, host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+from trajectory_generation_amd import batch as TB  # noqa: E402
+from trajectory_generation_amd.workload import make_workload  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def algorithmic_bytes_per_traj(N: int, kmax: int) -> int:
+    """Bytes one trajectory's closed-loop step must move (DESIGN.md 'Roofline'):
+    reads  x 6, u_prev 2, vref N+1, path: kind (4 B) + pc 4 + nk (4 B) + knots kmax + coef 4(kmax-1)
+    writes x 6, u_prev 2, hist_x 6, hist_u 2, status (4 B), iters (4 B)."""
+    doubles = 6 + 2 + (N + 1) + 4 + kmax + 4 * (kmax - 1) + 6 + 2 + 6 + 2
+    return 8 * doubles + 4 * 4
+
+
+def cpu_baseline(w, N, Ts, ntraj, nsteps):
+    """The oracle (oracle/, C restatement of the reference path + OSQP's ADMM) on host cores."""
+    import oracle as O  # test infrastructure: used here only for the CPU-baseline leg
+    from trajectory_generation_amd.batch import spline_natural
+    O.build()
+    paths = []
+    for k, c, kn in zip(w["kinds"][:ntraj], w["pcs"][:ntraj], w["knots"][:ntraj]):
+        if k == 2:
+            paths.append(O.Path(2, (0, 0, 0, 0), xk=kn[0], coef=spline_natural(kn[0], kn[1]).reshape(-1)))
+        else:
+            paths.append(O.Path(int(k), c))
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cfg = O.cfg(N=N, Ts=Ts)
+    t0 = time.perf_counter()
+    O.closed_loop_batch(paths, w["x0"][:ntraj], w["u0"][:ntraj], w["vref"], nsteps, cfg, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=ntraj * nsteps / dt, unit="MPC steps/s", cores=threads, kind="port",
+                sample=f"{ntraj} trajectories x {nsteps} closed-loop steps (N={N}, dt={Ts}), "
+                       f"C oracle (OpenMP, {threads} threads) = restated mpc_6stati.py + OSQP ADMM/polish, "
+                       f"{dt:.2f} s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
+    ap.add_argument("--horizon", type=int, default=20)
+    ap.add_argument("--dt", type=float, default=0.05)
+    ap.add_argument("--kind", default="spline", choices=["spline", "mixed", "parabola"])
+    ap.add_argument("--polish-mode", type=int, default=0)
+    ap.add_argument("--cpu-traj", type=int, default=1024)
+    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
+                    help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = TB.require_gpu(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    N, Ts, B = args.horizon, args.dt, args.batch
+    w = make_workload(B, N, Ts, kind=args.kind, seed=0, id_offset=rank * B)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=dev)
+    x = torch.as_tensor(w["x0"], device=dev).contiguous()
+    u = torch.as_tensor(w["u0"], device=dev).contiguous()
+    vref = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=dev).contiguous()
+    cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=args.polish_mode)
+    T = args.warmup + args.steps
+    hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=dev)
+    hu = torch.empty((B, T, 2), dtype=torch.float64, device=dev)
+    hx[:, 0] = x
+    st = torch.empty((T, B), dtype=torch.int32, device=dev)
+    it = torch.empty((T, B), dtype=torch.int32, device=dev)
+
+    for t in range(args.warmup):
+        TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        t = args.warmup + k
+        ev[k][0].record()
+        TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    iters = it[args.warmup:].cpu().numpy().reshape(-1)
+    stat = st[args.warmup:].cpu().numpy().reshape(-1)
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    total = world * B * args.steps
+    value = total / elapsed
+    kmax = int(paths.xk.shape[1])
+    bytes_launch = B * algorithmic_bytes_per_traj(N, kmax)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("batch") == B and tj.get("horizon") == N:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    out = {
+        "metric": "MPC steps/sec (batch=4096, N=20)" if (B == 4096 and N == 20) else f"MPC steps/sec (batch={B}, N={N})",
+        "value": value,
+        "unit": "MPC steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": f"closed-loop {args.kind}-tracking MPC, {B} trajectories/GPU, N={N}, dt={Ts}s",
+                   "global_batch": world * B, "horizon": N, "dt": Ts, "parallelism": f"shard{world}",
+                   "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "mpc_step_kernel<40,true,true> (traj_closed_loop_step)",
+                     "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch},
+        "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
+                         "iters_max": int(iters.max()),
+                         "status_hist": np.bincount(stat, minlength=7).tolist()},
+    }
+    if not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(w, N, Ts, min(args.cpu_traj, B), args.cpu_steps)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -103,6 +103,8 @@ def lib():
         L.orc_spline_natural.argtypes = [C.c_int, _D, _D, _D]
         L.orc_closed_loop.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), C.POINTER(OrcPath), _D, _D, _D,
                                       C.c_int, _D, _D, _I, _I]
+        L.orc_closed_loop_batch.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), C.POINTER(OrcPath), C.c_int,
+                                            _D, _D, _D, C.c_int, _D, _D, _I, _I, C.c_int]
         _lib = L
     return _lib
 
@@ -301,4 +303,17 @@ def closed_loop(path: Path, x0, u0, vref, T, c: OrcCfg, p=None):
     it = np.zeros(T, np.int32)
     lib().orc_closed_loop(C.byref(p), C.byref(c), C.byref(path.s), _dp(_f64(x0, 6)), _dp(_f64(u0, 2)),
                           _dp(_f64(vref, c.N + 1)), int(T), _dp(tx), _dp(tu), _ip(st), _ip(it))
+    return dict(X=tx, U=tu, status=st, iters=it)
+
+
+def closed_loop_batch(paths: list, x0, u0, vref, T, c: OrcCfg, p=None, nthreads=0):
+    """B closed loops with OpenMP over trajectories; paths is a list of Path."""
+    p = p or params()
+    B = len(paths)
+    arr = (OrcPath * B)(*[pa.s for pa in paths])
+    x0 = _f64(x0, (B, 6)); u0 = _f64(u0, (B, 2))
+    tx = np.zeros((B, T + 1, 6)); tu = np.zeros((B, T, 2))
+    st = np.zeros((B, T), np.int32); it = np.zeros((B, T), np.int32)
+    lib().orc_closed_loop_batch(C.byref(p), C.byref(c), arr, B, _dp(x0), _dp(u0), _dp(_f64(vref, c.N + 1)), int(T),
+                                _dp(tx), _dp(tu), _ip(st), _ip(it), int(nthreads))
     return dict(X=tx, U=tu, status=st, iters=it)

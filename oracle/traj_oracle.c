@@ -1208,3 +1208,16 @@ void orc_closed_loop(const orc_params* p, const orc_mpc_cfg* c, const orc_path* 
     }
     free(pref);
 }
+
+void orc_closed_loop_batch(const orc_params* p, const orc_mpc_cfg* c, const orc_path* paths, int B,
+                           const double* x0, const double* u0, const double* vref, int T, double* traj_x,
+                           double* traj_u, int* status, int* iters, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1)
+#endif
+    for (int b = 0; b < B; ++b)
+        orc_closed_loop(p, c, paths + b, x0 + 6 * b, u0 + 2 * b, vref, T, traj_x + (size_t)6 * (T + 1) * b,
+                        traj_u + (size_t)2 * T * b, status ? status + (size_t)T * b : NULL,
+                        iters ? iters + (size_t)T * b : NULL);
+}

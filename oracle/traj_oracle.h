@@ -144,6 +144,12 @@ void orc_closed_loop(const orc_params* p, const orc_mpc_cfg* c, const orc_path* 
                      const double u0[2], const double* vref, int T, double* traj_x, double* traj_u,
                      int* status, int* iters);
 
+/* B independent closed loops (OpenMP over trajectories): paths[B], x0 [B,6], u0 [B,2], vref (N+1)
+ * shared; traj_x [B,T+1,6], traj_u [B,T,2], status [B,T], iters [B,T] (status/iters may be NULL). */
+void orc_closed_loop_batch(const orc_params* p, const orc_mpc_cfg* c, const orc_path* paths, int B,
+                           const double* x0, const double* u0, const double* vref, int T, double* traj_x,
+                           double* traj_u, int* status, int* iters, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif
