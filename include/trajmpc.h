@@ -25,12 +25,14 @@
  *   - All array pointers are DEVICE pointers (hipMalloc / torch.cuda memory), row-major, float64
  *     (the reference computes in numpy float64).  Shapes are given per argument.
  *   - `stream` is a hipStream_t (NULL = default stream).  Calls are asynchronous; they never
- *     allocate, copy to the host or synchronize, so they can be captured in a hipGraph.
+ *     allocate, copy to the host or synchronize, so they can be captured in a hipGraph.  Scratch
+ *     memory is the caller's `workspace` (size from traj_mpc_workspace_bytes).
  *   - Return value: 0 on success, negative TRAJ_E_* on argument / launch errors.
  *   - Per-instance solver outcome is written to `status` (TRAJ_STATUS_*, same numbering as the
  *     CVXPY status strings listed below).  Like mpc_6stati.py:257-262, an instance whose status
  *     is not OPTIMAL / OPTIMAL_INACCURATE gets u_cmd = u_prev and NaN in X_opt / U_opt / objective.
- *   - Ownership: the caller owns every buffer.  The library holds no global state.
+ *   - Ownership: the caller owns every buffer.  The library holds no global state (except the
+ *     diagnostics pointer of traj_debug_set_stamps).
  *   - Thread safety: reentrant; use one stream per host thread.
  */
 #ifndef TRAJMPC_H
@@ -80,6 +82,8 @@ typedef struct {
     int polish_max_pass;
     double cert_tol;
     int polish_max_rounds;
+    int warm_start;                   /* closed loop: start ADMM from the previous step's shifted
+                                       * solution (mpc_6stati.py:256 requests warm_start=True) */
 } traj_mpc_config;
 
 #define TRAJ_MAX_N 40
@@ -106,14 +110,21 @@ int traj_linearize_discretize_batch(const traj_vehicle_params* p, int B, double 
 int traj_lateral_error_batch(int B, const double* X, const double* Y, const double* Xref, const double* Yref,
                              const double* phiref, double* out /*[B]*/, void* stream);
 
+/* Device workspace the MPC step needs for B instances of horizon N: the linearization A_k, B_k, g_k
+ * handed from the linearize kernel to the solve kernel (B * N * 54 doubles) followed by the
+ * closed-loop warm-start state (B * (6 N + 2) doubles).  Pass the same buffer to every
+ * traj_closed_loop_step of one run; step t = 0 starts cold. */
+size_t traj_mpc_workspace_bytes(int B, int N);
+
 /* ---- the MPC step (mpc_6stati.py:120-275) for B independent instances ----
  * x0 [B,6], u_prev [B,2], path_ref [B,N+1,3], vref [B,N+1]  (vref None / scalar is expanded by the
  * caller, :155-160).  Outputs: u_cmd [B,2], status [B]; optional (may be NULL): objective [B],
- * X_opt [B,6,N+1], U_opt [B,2,N], iters [B] (ADMM iterations), polished [B] (1 if polish accepted). */
+ * X_opt [B,6,N+1], U_opt [B,2,N], iters [B] (ADMM iterations), polished [B] (1 if polish accepted).
+ * workspace: device buffer of at least traj_mpc_workspace_bytes(B, N) bytes. */
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                         const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
                         int* status, double* objective, double* X_opt, double* U_opt, int* iters, int* polished,
-                        void* stream);
+                        void* workspace, size_t workspace_bytes, void* stream);
 
 /* QP half only (mpc_6stati.py:180-275) with the linearization supplied by the caller:
  * Ad [B,N,6,6], Bd [B,N,6,2], g [B,N,6].  Same outputs as traj_mpc_step_batch. */
@@ -148,7 +159,15 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
  * status / iters [B] (optional) receive this step's solver outcome. */
 int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
                           double* x, double* u_prev, const double* vref, int t, int hist_T, double* hist_x,
-                          double* hist_u, int* status, int* iters, void* stream);
+                          double* hist_u, int* status, int* iters, void* workspace, size_t workspace_bytes,
+                          void* stream);
+
+/* ---- diagnostics ----
+ * Subsequent MPC launches write, per instance b, 16 int64 slots at buf[16 b ..] (device memory):
+ * [0..7] s_memtime at phase boundaries (start, inputs, rollout, linearization, condensing,
+ * scaling, solver end, outputs), [8] KKT factorizations, [9] ADMM iterations, [10] polish passes.
+ * NULL disables.  For profiling only; never enabled by the product path. */
+int traj_debug_set_stamps(long long* buf);
 
 #ifdef __cplusplus
 }

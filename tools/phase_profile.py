@@ -1,0 +1,42 @@
+"""Per-phase cycle breakdown of the fused MPC kernel (uses traj_debug_set_stamps; diagnostics only)."""
+import sys, os, ctypes as C
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from trajectory_generation_amd import batch as TB, _lib
+from trajectory_generation_amd.workload import make_workload
+
+def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
+    dev = TB.require_gpu()
+    w = make_workload(B, N, Ts, kind=kind)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    x = torch.as_tensor(w["x0"], device=dev).contiguous(); u = torch.as_tensor(w["u0"], device=dev).contiguous()
+    vref = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=dev).contiguous()
+    cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
+    for t in range(warm):
+        TB.closed_loop_step(x, u, paths, vref, cfg)
+    dbg = torch.zeros((B, 16), dtype=torch.int64, device=dev)
+    _lib.lib().traj_debug_set_stamps(C.c_void_p(dbg.data_ptr()))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(); TB.closed_loop_step(x, u, paths, vref, cfg); e1.record()
+    torch.cuda.synchronize()
+    _lib.lib().traj_debug_set_stamps(None)
+    d = dbg.cpu().numpy()
+    names = ["inputs", "rollout", "linearize", "condense", "scale", "solve", "outputs"]
+    ph = np.diff(d[:, :8], axis=1)
+    print(f"kernel {e0.elapsed_time(e1):.3f} ms  B={B} N={N} kind={kind} polish_mode={polish_mode}")
+    print("phase       median      p90       max   (cycles)")
+    for i, nm in enumerate(names):
+        print(f"{nm:10s} {np.median(ph[:, i]):9.0f} {np.percentile(ph[:, i], 90):9.0f} {ph[:, i].max():9.0f}")
+    tot = d[:, 7] - d[:, 0]
+    print(f"{'total':10s} {np.median(tot):9.0f} {np.percentile(tot, 90):9.0f} {tot.max():9.0f}")
+    it, nf, ps = d[:, 9], d[:, 8], d[:, 10]
+    print("iters median", np.median(it), "p99", np.percentile(it, 99), "max", it.max(), " factorizations median", np.median(nf), "max", nf.max())
+    solve = ph[:, 5]
+    A = np.stack([it, nf, np.ones_like(it)], 1).astype(float)
+    coef, *_ = np.linalg.lstsq(A, solve.astype(float), rcond=None)
+    print("solve cycles ~ %.0f/iter + %.0f/factorization + %.0f" % tuple(coef))
+    span = (d[:, 7].max() - d[:, 0].min())
+    print("first start -> last end: %.0f cycles; start spread %.0f" % (span, d[:, 0].max() - d[:, 0].min()))
+
+if __name__ == "__main__":
+    main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0)

@@ -55,7 +55,7 @@ class MpcConfig(C.Structure):
         ("polish", C.c_int), ("polish_refine_iter", C.c_int), ("adaptive_rho", C.c_int),
         ("adaptive_rho_tol", C.c_double),
         ("polish_mode", C.c_int), ("polish_max_pass", C.c_int), ("cert_tol", C.c_double),
-        ("polish_max_rounds", C.c_int),
+        ("polish_max_rounds", C.c_int), ("warm_start", C.c_int),
     ]
 
 
@@ -78,13 +78,15 @@ _SIGS = {
     "traj_linearize_discretize_batch": (C.c_int, [C.POINTER(VehicleParams), C.c_int, C.c_double, _V, _V, _V, _V,
                                                   _V, _V]),
     "traj_lateral_error_batch": (C.c_int, [C.c_int, _V, _V, _V, _V, _V, _V, _V]),
+    "traj_mpc_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
     "traj_mpc_step_batch": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.c_int, _V, _V, _V, _V,
-                                      _V, _V, _V, _V, _V, _V, _V, _V]),
+                                      _V, _V, _V, _V, _V, _V, _V, _V, C.c_size_t, _V]),
     "traj_mpc_qp_batch": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.c_int, _V, _V, _V, _V, _V,
                                     _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_ref_window_batch": (C.c_int, [C.POINTER(Paths), C.c_int, C.c_int, C.c_double, _V, _V, _V, _V]),
+    "traj_debug_set_stamps": (C.c_int, [_V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,
-                                        _V, _V, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V]),
+                                        _V, _V, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V, C.c_size_t, _V]),
 }
 
 _lib = None

@@ -150,6 +150,20 @@ def _outputs(B, N, device):
                 polished=torch.empty(B, dtype=torch.int32, device=device))
 
 
+_WS = {}
+
+
+def workspace(B: int, N: int, device) -> torch.Tensor:
+    """Cached device workspace for B instances of horizon N (traj_mpc_workspace_bytes)."""
+    nbytes = int(_lib.lib().traj_mpc_workspace_bytes(int(B), int(N)))
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() * 8 < nbytes:
+        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+        _WS[key] = ws
+    return ws
+
+
 def mpc_step_batch(x0, u_prev, path_ref, vref, cfg: MpcConfig, params=None, out: dict | None = None) -> dict:
     """B independent mpc_step calls (mpc_6stati.py:120-275) in one launch.
 
@@ -164,10 +178,11 @@ def mpc_step_batch(x0, u_prev, path_ref, vref, cfg: MpcConfig, params=None, out:
     path_ref = _dev(path_ref, (B, N + 1, 3), dev)
     vref = _dev(vref, (B, N + 1), dev)
     o = out if out is not None else _outputs(B, N, dev)
+    ws = workspace(B, N, dev)
     _lib.check(_lib.lib().traj_mpc_step_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), _p(u_prev), _p(path_ref), _p(vref),
         _p(o["u_cmd"]), _p(o["status"]), _p(o["objective"]), _p(o["X_opt"]), _p(o["U_opt"]), _p(o["iters"]),
-        _p(o["polished"]), _stream()), "traj_mpc_step_batch")
+        _p(o["polished"]), _p(ws), ws.numel() * 8, _stream()), "traj_mpc_step_batch")
     return o
 
 
@@ -290,9 +305,10 @@ def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=Non
     B = x.shape[0]
     ps = paths.struct()
     T = hist_u.shape[1] if hist_u is not None else 0
+    ws = workspace(B, cfg.N, x.device)
     _lib.check(_lib.lib().traj_closed_loop_step(
         C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t), int(T),
-        _p(hist_x), _p(hist_u), _p(status), _p(iters), _stream()), "traj_closed_loop_step")
+        _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()), "traj_closed_loop_step")
 
 
 def run_closed_loop(x0, u0, paths: PathSet, vref, T, cfg: MpcConfig, params=None, record=True) -> dict:

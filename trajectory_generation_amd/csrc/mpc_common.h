@@ -1,0 +1,144 @@
+// mpc_common.h -- shared definitions of the batched MPC step kernels for gfx950 (mpc_linearize.h,
+// mpc_solve.h).
+//
+// Reference hot path: MPC/mpc_6stati.py:120-275 (mpc_step).  Per instance the kernel runs
+//   1. nominal rollout          :165-172  x_{k+1} = x_k + Ts f(x_k, u_prev)
+//   2. linearize/discretize     :175-178  central differences (:73-97), A = I + Ts Jx, B = Ts Ju,
+//                                          g = x + Ts f - A x - B u (:99-109)
+//   3. the TV-LQ QP             :180-250  condensed over U (X eliminated by the dynamics)
+//   4. the solve                :252-262  OSQP's ADMM (Ruiz scaling, sigma/alpha, adaptive rho,
+//                                          OSQP termination) + polish, as restated in oracle/
+//   5. status / info            :257-275  u_cmd = U[:,0] or u_prev; X_opt by the linear model
+//
+// Layout (DESIGN.md "Kernel"): thread i (< n = 2N) owns QP variable i = 2k + channel, its box row
+// and its rate row.  Matrices live ROW-PER-LANE in registers: the KKT matrix
+// K = P + sigma I + A' diag(rho) A is inverted in place by the symmetric sweep operator
+// (n pivots, each a broadcast of one column through LDS), so every ADMM iteration is one dense
+// register mat-vec (n FMAs/lane) plus two +-2 neighbour exchanges for the banded constraint rows.
+// The scaled cost matrix P (needed for residuals, rho updates and polish) stays in LDS.
+// Everything is float64, like the reference.
+#pragma once
+#include "physics.h"
+
+namespace tgmpc {
+
+constexpr double INFTY = 1e30;
+constexpr double DIV_TOL = 1e-30;
+constexpr double MIN_SCALING = 1e-4;
+constexpr double MAX_SCALING = 1e4;
+constexpr double RHO_MIN = 1e-6;
+constexpr double RHO_MAX = 1e6;
+constexpr double RHO_TOL = 1e-4;
+constexpr double RHO_EQ_OVER_INEQ = 1e3;
+
+struct PathArgs {
+    int kmax;
+    const int* kind;
+    const double* pc;
+    const int* nk;
+    const double* xk;
+    const double* coef;
+};
+
+struct KArgs {
+    traj_vehicle_params p;
+    traj_mpc_config c;
+    int B;
+    const double* x0;        // [B,6]  (closed loop: state, updated in place)
+    const double* u_prev;    // [B,2]
+    const double* path_ref;  // [B,N+1,3] (unused in closed loop)
+    const double* vref;      // [B,N+1]
+    const double* Ad;        // [B,N,6,6] (QP-only mode)
+    const double* Bd;
+    const double* gd;
+    double* u_cmd;           // [B,2]
+    int* status;
+    double* objective;
+    double* X_opt;           // [B,6,N+1]
+    double* U_opt;           // [B,2,N]
+    int* iters;
+    int* polished;
+    // closed loop
+    PathArgs path;
+    double* x_state;         // [B,6]
+    double* u_state;         // [B,2]
+    int t, hist_T;
+    double* hist_x;          // [B,T+1,6]
+    double* hist_u;          // [B,T,2]
+    long long* dbg;          // diagnostics: per-block phase stamps (s_memtime) + counters, or null
+    double* wsA;             // linearization outputs (workspace): [B,N,6,6], [B,N,6,2], [B,N,6]
+    double* wsB;
+    double* wsg;
+    double* wsWarm;          // closed loop: per instance [U (2N), y_box (2N), y_rate (2N), rho, valid]
+};
+
+__device__ __forceinline__ double limit_scaling(double v) {
+    return v < MIN_SCALING ? 1.0 : (v > MAX_SCALING ? MAX_SCALING : v);
+}
+
+// reference path y(x), dy/dx for the closed-loop window (DESIGN.md "reference paths")
+__device__ inline void path_eval(const PathArgs& pa, int b, double x, double& y, double& dy) {
+    int kind = pa.kind[b];
+    const double* c = pa.pc + 4 * b;
+    if (kind == 0) {
+        y = c[0] + x * (c[1] + x * (c[2] + x * c[3]));
+        dy = c[1] + x * (2.0 * c[2] + x * 3.0 * c[3]);
+    } else if (kind == 1) {
+        double a = c[1] * x + c[2];
+        double s, co;
+        sincos(a, &s, &co);
+        y = c[0] * s + c[3];
+        dy = c[0] * c[1] * co;
+    } else {
+        int nk = pa.nk[b];
+        const double* xk = pa.xk + (size_t)pa.kmax * b;
+        const double* cf = pa.coef + (size_t)(pa.kmax - 1) * 4 * b;
+        if (x <= xk[0]) {
+            y = cf[0] + cf[1] * (x - xk[0]);
+            dy = cf[1];
+        } else if (x >= xk[nk - 1]) {
+            const double* q = cf + 4 * (nk - 2);
+            double h = xk[nk - 1] - xk[nk - 2];
+            double ye = q[0] + h * (q[1] + h * (q[2] + h * q[3]));
+            double se = q[1] + h * (2.0 * q[2] + h * 3.0 * q[3]);
+            y = ye + se * (x - xk[nk - 1]);
+            dy = se;
+        } else {
+            int j = 0;
+            while (j < nk - 2 && x >= xk[j + 1]) ++j;
+            const double* q = cf + 4 * j;
+            double tt = x - xk[j];
+            y = q[0] + tt * (q[1] + tt * (q[2] + tt * q[3]));
+            dy = q[1] + tt * (2.0 * q[2] + tt * 3.0 * q[3]);
+        }
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void wave_max(double (&v)[V]) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            double o = __shfl_xor(v[i], off, 64);
+            v[i] = (o > v[i] || o != o) ? o : v[i];
+        }
+    }
+}
+
+// a wave-uniform double moved to SGPRs (readfirstlane), so the compiler stops carrying it in VGPRs
+__device__ __forceinline__ double uniformize(double v) {
+    const long long bits = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readfirstlane((int)(bits & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(bits >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+
+}  // namespace tgmpc

@@ -1,153 +1,41 @@
-// mpc_kernel.h -- the fused batched MPC step for gfx950: one workgroup per trajectory instance.
+// mpc_solve.h -- kernel 2 of the MPC step: condensed TV-LQ QP + OSQP-style ADMM + polish.
 //
-// Reference hot path: MPC/mpc_6stati.py:120-275 (mpc_step).  Per instance the kernel runs
-//   1. nominal rollout          :165-172  x_{k+1} = x_k + Ts f(x_k, u_prev)
-//   2. linearize/discretize     :175-178  central differences (:73-97), A = I + Ts Jx, B = Ts Ju,
-//                                          g = x + Ts f - A x - B u (:99-109)
+// Reference hot path: MPC/mpc_6stati.py:180-275 (QP build, prob.solve(OSQP), status, info), with
+// the linearization (A_k, B_k, g_k) produced by mpc_linearize.h (or given by the caller for
+// traj_mpc_qp_batch) and read from global memory.
 //   3. the TV-LQ QP             :180-250  condensed over U (X eliminated by the dynamics)
 //   4. the solve                :252-262  OSQP's ADMM (Ruiz scaling, sigma/alpha, adaptive rho,
 //                                          OSQP termination) + polish, as restated in oracle/
 //   5. status / info            :257-275  u_cmd = U[:,0] or u_prev; X_opt by the linear model
 //
 // Layout (DESIGN.md "Kernel"): thread i (< n = 2N) owns QP variable i = 2k + channel, its box row
-// and its rate row.  Matrices live ROW-PER-LANE in registers: the KKT matrix
-// K = P + sigma I + A' diag(rho) A is inverted in place by the symmetric sweep operator
-// (n pivots, each a broadcast of one column through LDS), so every ADMM iteration is one dense
-// register mat-vec (n FMAs/lane) plus two +-2 neighbour exchanges for the banded constraint rows.
-// The scaled cost matrix P (needed for residuals, rho updates and polish) stays in LDS.
+// and its rate row.  The KKT matrix K = P + sigma I + A' diag(rho) A lives ROW-PER-LANE in
+// registers and is inverted in place by the symmetric sweep operator (n pivots, each a broadcast
+// of one column through LDS), so every ADMM iteration is one dense register mat-vec (n FMAs per
+// lane) plus two +-2 neighbour exchanges for the banded constraint rows.  The scaled cost matrix P
+// (needed for residuals, rho updates and polish) is kept in LDS as a packed upper triangle.
 // Everything is float64, like the reference.
 #pragma once
-#include "physics.h"
+#include "mpc_common.h"
 
 namespace tgmpc {
 
-constexpr double INFTY = 1e30;
-constexpr double DIV_TOL = 1e-30;
-constexpr double MIN_SCALING = 1e-4;
-constexpr double MAX_SCALING = 1e4;
-constexpr double RHO_MIN = 1e-6;
-constexpr double RHO_MAX = 1e6;
-constexpr double RHO_TOL = 1e-4;
-constexpr double RHO_EQ_OVER_INEQ = 1e3;
-
-struct PathArgs {
-    int kmax;
-    const int* kind;
-    const double* pc;
-    const int* nk;
-    const double* xk;
-    const double* coef;
-};
-
-struct KArgs {
-    traj_vehicle_params p;
-    traj_mpc_config c;
-    int B;
-    const double* x0;        // [B,6]  (closed loop: state, updated in place)
-    const double* u_prev;    // [B,2]
-    const double* path_ref;  // [B,N+1,3] (unused in closed loop)
-    const double* vref;      // [B,N+1]
-    const double* Ad;        // [B,N,6,6] (QP-only mode)
-    const double* Bd;
-    const double* gd;
-    double* u_cmd;           // [B,2]
-    int* status;
-    double* objective;
-    double* X_opt;           // [B,6,N+1]
-    double* U_opt;           // [B,2,N]
-    int* iters;
-    int* polished;
-    // closed loop
-    PathArgs path;
-    double* x_state;         // [B,6]
-    double* u_state;         // [B,2]
-    int t, hist_T;
-    double* hist_x;          // [B,T+1,6]
-    double* hist_u;          // [B,T,2]
-};
-
-__device__ __forceinline__ double limit_scaling(double v) {
-    return v < MIN_SCALING ? 1.0 : (v > MAX_SCALING ? MAX_SCALING : v);
-}
-
-// reference path y(x), dy/dx for the closed-loop window (DESIGN.md "reference paths")
-__device__ inline void path_eval(const PathArgs& pa, int b, double x, double& y, double& dy) {
-    int kind = pa.kind[b];
-    const double* c = pa.pc + 4 * b;
-    if (kind == 0) {
-        y = c[0] + x * (c[1] + x * (c[2] + x * c[3]));
-        dy = c[1] + x * (2.0 * c[2] + x * 3.0 * c[3]);
-    } else if (kind == 1) {
-        double a = c[1] * x + c[2];
-        double s, co;
-        sincos(a, &s, &co);
-        y = c[0] * s + c[3];
-        dy = c[0] * c[1] * co;
-    } else {
-        int nk = pa.nk[b];
-        const double* xk = pa.xk + (size_t)pa.kmax * b;
-        const double* cf = pa.coef + (size_t)(pa.kmax - 1) * 4 * b;
-        if (x <= xk[0]) {
-            y = cf[0] + cf[1] * (x - xk[0]);
-            dy = cf[1];
-        } else if (x >= xk[nk - 1]) {
-            const double* q = cf + 4 * (nk - 2);
-            double h = xk[nk - 1] - xk[nk - 2];
-            double ye = q[0] + h * (q[1] + h * (q[2] + h * q[3]));
-            double se = q[1] + h * (2.0 * q[2] + h * 3.0 * q[3]);
-            y = ye + se * (x - xk[nk - 1]);
-            dy = se;
-        } else {
-            int j = 0;
-            while (j < nk - 2 && x >= xk[j + 1]) ++j;
-            const double* q = cf + 4 * j;
-            double tt = x - xk[j];
-            y = q[0] + tt * (q[1] + tt * (q[2] + tt * q[3]));
-            dy = q[1] + tt * (2.0 * q[2] + tt * 3.0 * q[3]);
-        }
-    }
-}
-
-template <int V>
-__device__ __forceinline__ void wave_max(double (&v)[V]) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-        for (int i = 0; i < V; ++i) {
-            double o = __shfl_xor(v[i], off, 64);
-            v[i] = (o > v[i] || o != o) ? o : v[i];
-        }
-    }
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
 // =====================================================================================
-// The kernel.  NN = capacity in QP variables (>= 2N), LIN = compute the linearization (else read
-// Ad/Bd/g), CLOSED = closed-loop step (window from the state, plant update, history).
+// NN = capacity in QP variables (>= 2N); CLOSED = closed-loop step (window from the state, plant
+// update, history).  A_k, B_k, g_k are read from a.Ad / a.Bd / a.gd ([B,N,36], [B,N,12], [B,N,6]).
 // =====================================================================================
-template <int NN, bool LIN, bool CLOSED>
-__global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const KArgs a) {
+template <int NN, bool CLOSED>
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArgs a) {
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
-    constexpr int PS = NN + 1;          // padded row stride of P in LDS
-    constexpr int NFD = 12;             // FD perturbations per stage (vars 2..5 and u, +/-)
-    constexpr int BIG = (NM * NFD * 6 > NN * PS) ? NM * NFD * 6 : NN * PS;
+    constexpr int NP = NN * (NN + 1) / 2;
 
     __shared__ double s_pref[3 * (NM + 1)];
     __shared__ double s_vref[NM + 1];
     __shared__ double s_x0[6], s_up[2];
-    __shared__ double s_xbar[(NM + 1) * 6];
-    __shared__ double s_fbar[NM * 6];
-    __shared__ double s_A[NM * 36];
-    __shared__ double s_B[NM * 12];
-    __shared__ double s_g[NM * 6];
-    __shared__ double s_big[BIG];       // FD outputs, then the scaled P (row stride PS)
+    __shared__ double s_P[NP];          // scaled P, packed upper triangle (row-major)
+    __shared__ double s_cold[8 * NT];   // per-lane values used only off the ADMM hot path
     __shared__ double s_xh[(NM + 1) * 6];
     __shared__ double s_sc[(NM + 1) * 2];
     __shared__ double s_e[(NM + 1) * 3];
@@ -165,6 +53,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
     const bool own = t < n;             // owns variable / rows t
     const int kk = t >> 1, ch = t & 1;  // stage and channel of variable t
     int xb = 0;                         // rotating exchange buffer
+    auto stamp = [&](int i, long long v) {
+        if (a.dbg && t == 0) a.dbg[(size_t)b * 16 + i] = v;
+    };
+    stamp(0, __builtin_amdgcn_s_memtime());
 
     // ---- block helpers -------------------------------------------------------------
     auto exch = [&](double v, int delta) -> double {   // value of variable t+delta (0 outside)
@@ -182,9 +74,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
         __syncthreads();
         return buf;
     };
-    auto block_max = [&](auto& v) {                   // in-place max over the block
+    auto block_max = [&](auto& v) {                   // in-place max over the block (uniform result)
         constexpr int V = sizeof(v) / sizeof(double);
         wave_max<V>(v);
+        if (WAVES == 1)
+            for (int i = 0; i < V; ++i) v[i] = uniformize(v[i]);
         if (WAVES > 1) {
             if (lane == 0)
                 for (int i = 0; i < V; ++i) s_red[wid * V + i] = v[i];
@@ -199,6 +93,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
     };
     auto block_sum = [&](double v) -> double {
         v = wave_sum(v);
+        if (WAVES == 1) v = uniformize(v);
         if (WAVES > 1) {
             if (lane == 0) s_red[wid] = v;
             __syncthreads();
@@ -212,6 +107,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
 
     // ---- 0. inputs -----------------------------------------------------------------
     if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+    // exchange buffers start at zero: entries >= n are the zero padding the unguarded
+    // register loops over the full capacity NN rely on
+    for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
     if (CLOSED) {
         if (t < 6) s_x0[t] = a.x_state[6 * b + t];
         if (t < 2) s_up[t] = a.u_state[2 * b + t];
@@ -251,74 +149,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
         if (bad) s_flag[0] = 1;
     }
 
-    // ---- 1. nominal rollout (:165-172) ---------------------------------------------
-    if (t == 0) {
-        double x[6], f[6], sd, cd;
-        sincos(s_up[1], &sd, &cd);
-        for (int i = 0; i < 6; ++i) { x[i] = s_x0[i]; s_xbar[i] = x[i]; }
-        for (int k = 0; k < N; ++k) {
-            f_cont_sc(p, x, s_up[0], s_up[1], sd, cd, f);
-            for (int i = 0; i < 6; ++i) {
-                s_fbar[6 * k + i] = f[i];
-                x[i] = x[i] + Ts * f[i];
-                s_xbar[6 * (k + 1) + i] = x[i];
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- 2. linearization (:175-178 -> :73-109) ------------------------------------
-    if (LIN) {
-        const double eps = 1e-5;
-        for (int it = t; it < NFD * N; it += NT) {
-            int k = it / NFD, q = it % NFD;
-            double x[6], u[2], f[6];
-            for (int i = 0; i < 6; ++i) x[i] = s_xbar[6 * k + i];
-            u[0] = s_up[0];
-            u[1] = s_up[1];
-            double dd = (q & 1) ? -eps : eps;
-            // x + dx / x - dx with dx = eps e_j  (x_i + 0.0 elsewhere, as numpy does)
-            if (q < 8) {
-                int v = 2 + (q >> 1);
-                for (int i = 0; i < 6; ++i) x[i] = (q & 1) ? x[i] - (i == v ? eps : 0.0) : x[i] + (i == v ? eps : 0.0);
-                (void)dd;
-            } else {
-                int v = (q - 8) >> 1;
-                for (int i = 0; i < 2; ++i) u[i] = (q & 1) ? u[i] - (i == v ? eps : 0.0) : u[i] + (i == v ? eps : 0.0);
-            }
-            f_cont(p, x, u, f);
-            for (int i = 0; i < 6; ++i) s_big[(k * NFD + q) * 6 + i] = f[i];
-        }
-        __syncthreads();
-        // Jx columns 0,1 are exactly zero (f does not read X, Y: f(x+dx) - f(x-dx) == 0 bit for bit)
-        for (int it = t; it < 8 * N; it += NT) {
-            int k = it >> 3, col = it & 7;
-            for (int r = 0; r < 6; ++r) {
-                double J = 0.0;
-                if (col >= 2) {
-                    int q = (col - 2) * 2;   // perturbation index of (+) for this column (state 2..5, u 0..1)
-                    J = (s_big[(k * NFD + q) * 6 + r] - s_big[(k * NFD + q + 1) * 6 + r]) / (2.0 * eps);
-                }
-                if (col < 6) s_A[k * 36 + r * 6 + col] = ((r == col) ? 1.0 : 0.0) + Ts * J;
-                else s_B[k * 12 + r * 2 + (col - 6)] = Ts * J;
-            }
-        }
-        __syncthreads();
-        for (int it = t; it < 6 * N; it += NT) {
-            int k = it / 6, r = it % 6;
-            double ax = 0.0, bu = 0.0;
-            for (int cc = 0; cc < 6; ++cc) ax += s_A[k * 36 + r * 6 + cc] * s_xbar[6 * k + cc];
-            for (int cc = 0; cc < 2; ++cc) bu += s_B[k * 12 + r * 2 + cc] * s_up[cc];
-            s_g[6 * k + r] = s_xbar[6 * k + r] + Ts * s_fbar[6 * k + r] - ax - bu;
-        }
-    } else {
-        const size_t o = (size_t)b * N;
-        for (int i = t; i < 36 * N; i += NT) s_A[i] = a.Ad[o * 36 + i];
-        for (int i = t; i < 12 * N; i += NT) s_B[i] = a.Bd[o * 12 + i];
-        for (int i = t; i < 6 * N; i += NT) s_g[i] = a.gd[o * 6 + i];
-    }
-    __syncthreads();
-
+    stamp(1, __builtin_amdgcn_s_memtime());
+    const double* gA = a.Ad + (size_t)b * N * 36;   // this instance's linearization
+    const double* gB = a.Bd + (size_t)b * N * 12;
+    const double* gg = a.gd + (size_t)b * N * 6;
+    stamp(2, __builtin_amdgcn_s_memtime());
+    stamp(3, __builtin_amdgcn_s_memtime());
     // ---- 3. condensed QP (:180-250) --------------------------------------------------
     // free response xh_{k+1} = A_k xh_k + g_k
     if (t < 6) s_xh[t] = s_x0[t];
@@ -326,8 +162,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
     for (int k = 0; k < N; ++k) {
         if (t < 6) {
             double v = 0.0;
-            for (int cc = 0; cc < 6; ++cc) v += s_A[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
-            s_xh[6 * (k + 1) + t] = v + s_g[6 * k + t];
+            for (int cc = 0; cc < 6; ++cc) v += gA[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
+            s_xh[6 * (k + 1) + t] = v + gg[6 * k + t];
         }
         __syncthreads();
     }
@@ -361,12 +197,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
                     double Gn[6];
                     for (int r = 0; r < 6; ++r) {
                         double v = 0.0;
-                        for (int cc = 0; cc < 6; ++cc) v = fma(s_A[k * 36 + r * 6 + cc], G[cc], v);
+                        for (int cc = 0; cc < 6; ++cc) v = fma(gA[k * 36 + r * 6 + cc], G[cc], v);
                         Gn[r] = v;
                     }
                     for (int r = 0; r < 6; ++r) G[r] = Gn[r];
                 } else if (kk == k) {
-                    for (int r = 0; r < 6; ++r) G[r] = s_B[k * 12 + r * 2 + ch];
+                    for (int r = 0; r < 6; ++r) G[r] = gB[k * 12 + r * 2 + ch];
                 }
             }
             // output sensitivities of stage k+1: F = C_{k+1} G
@@ -376,13 +212,15 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
             xb++;
             if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
             __syncthreads();
-            if (own) {
-                double w0 = 2.0 * W0 * F0, w1 = 2.0 * W1 * F1, w2 = 2.0 * W2 * F2;
+            {
+                // P_tj += 2 W (F_t F_j): the product F_t F_j is symmetric in (t, j), so P stays
+                // bitwise symmetric; entries j >= n read the zero padding
+                const double w0 = 2.0 * W0, w1 = 2.0 * W1, w2 = 2.0 * W2;
                 const double* ek = s_e + 3 * (k + 1);
-                qi += w0 * ek[0] + w1 * ek[1] + w2 * ek[2];
+                qi += w0 * F0 * ek[0] + w1 * F1 * ek[1] + w2 * F2 * ek[2];
 #pragma unroll
                 for (int j = 0; j < NN; ++j)
-                    if (j < n) Prow[j] = fma(w0, buf[j], fma(w1, buf[NN + j], fma(w2, buf[2 * NN + j], Prow[j])));
+                    Prow[j] = fma(w0, F0 * buf[j], fma(w1, F1 * buf[NN + j], fma(w2, F2 * buf[2 * NN + j], Prow[j])));
             }
         }
         __syncthreads();
@@ -398,14 +236,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
         const double dmul = (kk < N - 1) ? 2.0 : 1.0;
 #pragma unroll
         for (int j = 0; j < NN; ++j) {
-            if (j < n) {
-                int kj = j >> 1;
-                double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
-                double add = 0.0;
-                if (kj == kk) add = 2.0 * rs + 2.0 * rd * dmul;
-                else if (kj == kk - 1 || kj == kk + 1) add = -2.0 * rd;
-                Prow[j] += add;
-            }
+            const int kj = j >> 1;
+            const double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
+            double add = (kj == kk) ? 2.0 * rs + 2.0 * rd * dmul : 0.0;
+            add = (j < n && (kj == kk - 1 || kj == kk + 1)) ? -2.0 * rd : add;
+            Prow[j] += add;
         }
         if (kk == 0) qi -= 2.0 * (Rd0 * s_up[0] + Rd1 * s_up[1]);
     }
@@ -421,8 +256,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
         if (own) {
             bad |= !isfinite(qi);
 #pragma unroll
-            for (int j = 0; j < NN; ++j)
-                if (j < n) bad |= !isfinite(Prow[j]);
+            for (int j = 0; j < NN; ++j) bad |= !isfinite(Prow[j]);
         }
         if (bad) s_flag[0] = 1;
     }
@@ -446,6 +280,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
     int status = TRAJ_STATUS_SOLVER_ERROR, iter = 0, pol = 0;
     double xsol = 0.0;  // unscaled U_t at exit
 
+    stamp(4, __builtin_amdgcn_s_memtime());
     if (early < 0) {
         // ---- 4a. Ruiz equilibration + cost scaling (OSQP scale_data) ---------------
         double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0;
@@ -455,18 +290,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
             double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
             double pn = 0.0;
 #pragma unroll
-            for (int j = 0; j < NN; ++j)
-                if (j < n) pn = fmax(pn, fabs(Prow[j]));
+            for (int j = 0; j < NN; ++j) pn = fmax(pn, fabs(Prow[j]));
             double coln = fmax(pn, fmax(fabs(a_b), fmax(fabs(a_r), fabs(a_rp))));
             double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
             double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
             double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
             double* Dv = bcast(Dt);
-            if (own) {
 #pragma unroll
-                for (int j = 0; j < NN; ++j)
-                    if (j < n) Prow[j] *= Dt * Dv[j];
-            }
+            for (int j = 0; j < NN; ++j) Prow[j] *= Dt * Dv[j];
             qi *= Dt;
             D *= Dt;
             Eb *= Etb;
@@ -474,34 +305,58 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
             // cost scaling
             double cn = 0.0;
 #pragma unroll
-            for (int j = 0; j < NN; ++j)
-                if (j < n) cn = fmax(cn, fabs(Prow[j]));
+            for (int j = 0; j < NN; ++j) cn = fmax(cn, fabs(Prow[j]));
             double mean = block_sum(own ? cn : 0.0) / n;
             double qv[1] = {own ? fabs(qi) : 0.0};
             block_max(qv);
             double ct = fmax(mean, limit_scaling(qv[0]));
             ct = 1.0 / limit_scaling(ct);
-            if (own) {
 #pragma unroll
-                for (int j = 0; j < NN; ++j) Prow[j] *= ct;
-            }
+            for (int j = 0; j < NN; ++j) Prow[j] *= ct;
             qi *= ct;
             cs *= ct;
         }
-        const double Dinv = 1.0 / D, Ebinv = 1.0 / Eb, Erinv = 1.0 / Er, csinv = 1.0 / cs;
+        const double csinv = 1.0 / cs;   // uniform
         const double D_dn = exch(D, -2), Er_up = exch(Er, +2);
         const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
         // scaled bounds
-        double slb = (lb > -INFTY) ? lb * Eb : -INFTY, sub = (ub < INFTY) ? ub * Eb : INFTY;
-        double slr = (lr > -INFTY) ? lr * Er : -INFTY, sur = (ur < INFTY) ? ur * Er : INFTY;
+        const double slb = (lb > -INFTY) ? lb * Eb : -INFTY, sub = (ub < INFTY) ? ub * Eb : INFTY;
+        const double slr = (lr > -INFTY) ? lr * Er : -INFTY, sur = (ur < INFTY) ? ur * Er : INFTY;
+        // Cold per-lane values go to LDS and are re-read (volatile: never hoisted into registers)
+        // where needed -- residual checks, the K build, polish -- keeping the ADMM loop's live set
+        // down to the inverse row + ~16 doubles.
+        enum { C_D = 0, C_EB, C_ER, C_LB, C_UB, C_LR, C_UR, C_ARUP };
+        {
+            const double a_r_up0 = exch(a_r, +2);
+            double* cw = s_cold + t;
+            cw[C_D * NT] = D; cw[C_EB * NT] = Eb; cw[C_ER * NT] = Er;
+            cw[C_LB * NT] = lb; cw[C_UB * NT] = ub; cw[C_LR * NT] = lr; cw[C_UR * NT] = ur;
+            cw[C_ARUP * NT] = a_r_up0;
+        }
+        auto cold = [&](int i) -> double { return ((volatile double*)s_cold)[i * NT + t]; };
         // scaled P to LDS (row stride PS)
-        if (own) {
+        // packed upper triangle: P(i, j), i <= j, at i*NN - i(i-1)/2 + (j - i); rows >= n are zero
+        if (t < NN) {
+            const int rt = t * NN - (t * (t - 1)) / 2 - t;
 #pragma unroll
             for (int j = 0; j < NN; ++j)
-                if (j < n) s_big[t * PS + j] = Prow[j];
+                if (j >= t) s_P[rt + j] = own ? Prow[j] : 0.0;
         }
         __syncthreads();
+        // Address of P(t, j) for a compile-time j: column segment (j < t) or row segment (j >= t).
+        // `opaque_t` re-materializes t through an asm move at each use site, so the compiler cannot
+        // hoist the NN per-lane addresses / compare masks out of the solver loops (that costs
+        // ~NN VGPRs + 2 NN SGPRs of loop-invariant state and spills everything else).
+        auto opaque_t = [&]() -> int {
+            int r;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t < NN ? t : 0));
+            return r;
+        };
+        auto paddr = [&](int j, int tt) -> int {
+            return (j < tt) ? (j * NN - (j * (j - 1)) / 2 - j + tt) : (tt * NN - (tt * (tt - 1)) / 2 - tt + j);
+        };
 
+        stamp(5, __builtin_amdgcn_s_memtime());
         // ---- helpers over the scaled problem ----------------------------------------
         // A x (box, rate) for the vector v owned row-wise
         auto Ax = [&](double v, double& zb, double& zr) {
@@ -514,26 +369,32 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
             double wr_up = exch(wr, +2);
             return a_b * wb + a_r * wr - a_rp * wr_up;
         };
-        auto Pmul = [&](double v) -> double {  // (P v)_t
+        auto Pmul = [&](double v) -> double {  // (P v)_t  (rows >= n are zero)
             double* vb = bcast(v);
-            double s = 0.0;
-            if (own) {
+            const int tt = opaque_t();
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
-                for (int j = 0; j < NN; ++j)
-                    if (j < n) s = fma(s_big[t * PS + j], vb[j], s);
+            for (int j = 0; j < NN; j += 4) {
+                s0 = fma(s_P[paddr(j, tt)], vb[j], s0);
+                if (j + 1 < NN) s1 = fma(s_P[paddr(j + 1, tt)], vb[j + 1], s1);
+                if (j + 2 < NN) s2 = fma(s_P[paddr(j + 2, tt)], vb[j + 2], s2);
+                if (j + 3 < NN) s3 = fma(s_P[paddr(j + 3, tt)], vb[j + 3], s3);
             }
-            return s;
+            return own ? (s0 + s1) + (s2 + s3) : 0.0;
         };
         double Krow[NN];
-        auto Kmul = [&](double v) -> double {
+        auto Kmul = [&](double v) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
             double* vb = bcast(v);
-            double s = 0.0;
-            if (own) {
+            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
 #pragma unroll
-                for (int j = 0; j < NN; ++j)
-                    if (j < n) s = fma(Krow[j], vb[j], s);
+            for (int j = 0; j < NN; j += 4) {
+                s0 = fma(Krow[j], vb[j], s0);
+                if (j + 1 < NN) s1 = fma(Krow[j + 1], vb[j + 1], s1);
+                if (j + 2 < NN) s2 = fma(Krow[j + 2], vb[j + 2], s2);
+                if (j + 3 < NN) s3 = fma(Krow[j + 3], vb[j + 3], s3);
+                if ((j & 7) == 4) __builtin_amdgcn_sched_barrier(0);   // bound live LDS values
             }
-            return s;
+            return own ? (s0 + s1) + (s2 + s3) : 0.0;
         };
         auto rho_for = [&](double l, double u, double rho) -> double {
             if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
@@ -550,6 +411,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
             double v[13];
             if (own) {
                 double dres = px + qi + aty;
+                const double Dinv = 1.0 / cold(C_D), Ebinv = 1.0 / cold(C_EB), Erinv = 1.0 / cold(C_ER);
                 v[0] = fmax(fabs(Ebinv * (axb - zb)), fabs(Erinv * (axr - zr)));   // prim res
                 v[1] = fmax(fabs(Ebinv * axb), fabs(Erinv * axr));
                 v[2] = fmax(fabs(Ebinv * zb), fabs(Erinv * zr));
@@ -589,15 +451,39 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
         constexpr int PH_ADMM = 0, PH_POLISH = 1, PH_DONE = 2;
         int phase = PH_ADMM;
         double rho = c.rho;
-        double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
         double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
+        // Warm start (closed loop, t > 0): the previous step's solution shifted one stage
+        // (receding horizon), mapped into this step's scaling.  mpc_6stati.py:256 asks OSQP for
+        // warm_start=True, which is a no-op there because a new Problem is built every call; the
+        // polished optimum does not depend on the starting point.
+        if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {
+            const double* wv = a.wsWarm + (size_t)b * (6 * N + 2);
+            if (wv[6 * N + 1] != 0.0) {
+                rho = fmin(fmax(wv[6 * N], RHO_MIN), RHO_MAX);
+                const int src = (kk < N - 1) ? t + 2 : t;          // shift one stage
+                const int srcm = (kk < N - 1) ? t : t - 2;         // previous variable of the rate row
+                if (own) {
+                    const double D = cold(C_D), Eb = cold(C_EB), Er = cold(C_ER);
+                    const double U = wv[src];
+                    const double Um = (kk == 0) ? s_up[ch] : wv[srcm];
+                    x = U / D;
+                    zb = clampd(Eb * U, slb, sub);
+                    zr = clampd(Er * (U - Um), slr, sur);
+                    const double yscale = cs;                      // y_scaled = c y / E
+                    yb = (kk < N - 1) ? yscale * wv[2 * N + src] / Eb : 0.0;
+                    yr = (kk < N - 1) ? yscale * wv[4 * N + src] / Er : 0.0;
+                }
+            }
+        }
+        double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
         Res r = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         int rounds = 0, ps = 0, actb = 0, actr = 0;
         double escale = 1.0;
         const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
-        const double a_r_up = exch(a_r, +2);
         iter = 1;
+        int nfact = 0;
         while (phase != PH_DONE) {
+            ++nfact;
             // ---- build K (row t) ----
             const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
             const double kr = (phase == PH_ADMM) ? rr : (actr ? 1.0 / dl : 0.0);
@@ -606,50 +492,67 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
                 const double kr_up = exch(kr, +2);
                 const double dii = ks + kb * a_b * a_b + kr * a_r * a_r + kr_up * a_rp * a_rp;
                 const double dm = -kr * a_r * a_rm;        // (t, t-2)
-                const double dp = -kr_up * a_r_up * a_rp;  // (t, t+2)
+                const double dp = -kr_up * cold(C_ARUP) * a_rp;  // (t, t+2)
+                const int tt = opaque_t();
 #pragma unroll
                 for (int j = 0; j < NN; ++j) {
-                    double v;
-                    if (own) {
-                        v = (j < n) ? s_big[t * PS + j] : 0.0;
-                        v += (j == t) ? dii : 0.0;
-                        v += (j == t - 2) ? dm : 0.0;
-                        v += (j == t + 2) ? dp : 0.0;
-                    } else {
-                        v = (j == t) ? 1.0 : 0.0;   // identity padding for rows n..NN-1
-                    }
+                    double v = own ? s_P[paddr(j, tt)] : 0.0;
+                    v += (j == tt) ? (own ? dii : 1.0) : 0.0;    // identity padding for rows n..NN-1
+                    v += (j == tt - 2) ? dm : 0.0;
+                    v += (j == tt + 2) ? dp : 0.0;
                     Krow[j] = v;
                 }
             }
-            // ---- sweep: Krow <- row t of K^{-1} (NN pivots, fully unrolled; padding pivots are 1) ----
+            // ---- sweep: Krow <- row t of K^{-1} (symmetric sweep operator, NN pivots) ----
+            // Rolled pivot loop with the row ROTATED so that the current pivot column is always
+            // register 0: before pivot pv, Krow[j] = K[t][(pv + j) mod NN] (after NN pivots the
+            // rotation is back to the identity).  Column pv is published twice (cb[t], cb[t + NN])
+            // so the pivot row in rotated order is the contiguous slice cb[pv .. pv + NN)
+            // (K symmetric: K[pv][c] = K[c][pv]).  Padding pivots (>= n) are identity and exact.
             bool ok = true;
-#pragma unroll
+#pragma nounroll
             for (int pv = 0; pv < NN; ++pv) {
-                double* cb = s_ex + (4 + (pv & 1)) * NN;
-                if (t < NN) cb[t] = Krow[pv];
+                double* cb = s_ex + (pv & 1) * 2 * NN;
+                if (t < NN) {
+                    cb[t] = Krow[0];
+                    cb[t + NN] = Krow[0];
+                }
                 __syncthreads();
-                const double d = cb[pv];
+                const double* prow = cb + pv;
+                const double d = prow[0];
                 ok = ok && (d > 0.0);
                 const double dinv = 1.0 / d;
-                if (t == pv) {
+                const bool piv = (t == pv);
+                const double fd = Krow[0] * dinv;
+                // K_tj <- al K_tj + be K_pj : (al, be) = (1, -K_tp/d) off the pivot row and (0, 1/d)
+                // on it (0 * K_tj is exact for finite K); column pv <- K_tp/d, or -1/d on the pivot
+                const double al = piv ? 0.0 : 1.0, be = piv ? dinv : -fd;
+                const double k0 = piv ? -dinv : fd;
 #pragma unroll
-                    for (int j = 0; j < NN; ++j)
-                        if (j != pv) Krow[j] = cb[j] * dinv;
-                    Krow[pv] = -dinv;
-                } else {
-                    const double fd = Krow[pv] * dinv;
-#pragma unroll
-                    for (int j = 0; j < NN; ++j)
-                        if (j != pv) Krow[j] = fma(-fd, cb[j], Krow[j]);
-                    Krow[pv] = fd;
-                }
+                for (int j = 1; j < NN; ++j) Krow[j - 1] = fma(be, prow[j], al * Krow[j]);
+                Krow[NN - 1] = k0;   // rotate: the pivot column moves to the end
             }
 #pragma unroll
             for (int j = 0; j < NN; ++j) Krow[j] = -Krow[j];
-            if (!ok) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
+            if (!ok) {
+                if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
+                // failed reduced-KKT factorization = unsuccessful polish (polish.c): the ADMM
+                // solution and status stand; exact mode continues ADMM like an uncertified pass
+                if (c.polish_mode == 1 && rounds < c.polish_max_rounds && iter < c.max_iter) {
+                    ++rounds;
+                    escale *= 1e-2;
+                    ++iter;
+                    phase = PH_ADMM;
+                } else {
+                    phase = PH_DONE;
+                }
+                continue;
+            }
 
             if (phase == PH_ADMM) {
                 bool converged = false, refactor = false;
+                const double rb_inv = 1.0 / rb, rr_inv = 1.0 / rr;
+                int chk = c.check_interval - (iter - 1) % c.check_interval;
                 for (; iter <= c.max_iter; ++iter) {
                     // rhs = sig x - q + A'(rho z - y)
                     double rhs = sig * x - qi + ATw(rb * zb - yb, rr * zr - yr);
@@ -659,14 +562,15 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
                     double xn = alpha * xt + (1.0 - alpha) * x;
                     double zrb = alpha * ztb + (1.0 - alpha) * zb;
                     double zrr = alpha * ztr + (1.0 - alpha) * zr;
-                    double vb = zrb + yb / rb, vr = zrr + yr / rr;
+                    double vb = zrb + rb_inv * yb, vr = zrr + rr_inv * yr;
                     double nzb = clampd(vb, slb, sub), nzr = clampd(vr, slr, sur);
                     yb = yb + rb * (zrb - nzb);
                     yr = yr + rr * (zrr - nzr);
                     x = xn;
                     zb = nzb;
                     zr = nzr;
-                    if (iter % c.check_interval == 0) {
+                    if (--chk == 0) {
+                        chk = c.check_interval;
                         r = residuals(x, zb, zr, yb, yr);
                         if (r.pr <= escale * r.eps_p && r.dr <= escale * r.eps_d) { converged = true; break; }
                         if (c.adaptive_rho) {
@@ -748,6 +652,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
                 double atyv = ATw(pyb, pyr);
                 const double tol = c.cert_tol;
                 double v[2];
+                const double Dinv = 1.0 / cold(C_D), Ebinv = 1.0 / cold(C_EB), Erinv = 1.0 / cold(C_ER);
+                const double lb = cold(C_LB), ub = cold(C_UB), lr = cold(C_LR), ur = cold(C_UR);
                 v[0] = own ? fabs(Dinv * (Pxv + qi + atyv)) * csinv : 0.0;            // stationarity
                 v[1] = own ? fmax(fabs(Dinv * qi), fabs(Dinv * Pxv)) * csinv : 0.0;  // gradient scale
                 block_max(v);
@@ -759,7 +665,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
                     if (sub < INFTY && axu > ub + tol * (1.0 + fabs(ub))) okc = 0;
                     if (slr > -INFTY && arv < lr - tol * (1.0 + fabs(lr))) okc = 0;
                     if (sur < INFTY && arv > ur + tol * (1.0 + fabs(ur))) okc = 0;
-                    double ybu = pyb * Eb * csinv, yru = pyr * Er * csinv;
+                    double ybu = pyb * cold(C_EB) * csinv, yru = pyr * cold(C_ER) * csinv;
                     if (actb < 0 && ybu > tol * gsc) okc = 0;
                     if (actb > 0 && ybu < -tol * gsc) okc = 0;
                     if (actr < 0 && yru > tol * gsc) okc = 0;
@@ -796,12 +702,29 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
             }
         }
         if (iter > c.max_iter) iter = c.max_iter;
-        xsol = D * x;
+        xsol = cold(C_D) * x;
+        if (CLOSED && a.wsWarm) {
+            double* wv = a.wsWarm + (size_t)b * (6 * N + 2);
+            const bool okst = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
+            if (own) {
+                wv[t] = xsol;
+                wv[2 * N + t] = yb * cold(C_EB) * csinv;   // unscaled y = E y / c
+                wv[4 * N + t] = yr * cold(C_ER) * csinv;
+            }
+            if (t == 0) {
+                wv[6 * N] = rho;
+                wv[6 * N + 1] = okst ? 1.0 : 0.0;
+            }
+        }
+        stamp(8, nfact);
+        stamp(10, ps);
     } else {
         status = early;
         iter = 0;
     }
 
+    stamp(6, __builtin_amdgcn_s_memtime());
+    stamp(9, iter);
     // ---- 5. outputs (:257-275) ------------------------------------------------------
     const bool good = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
     double* Ubuf = s_ex;  // U (stage-major) for the X rollout
@@ -814,8 +737,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
     for (int k = 0; k < N; ++k) {
         if (t < 6) {
             double v = 0.0;
-            for (int cc = 0; cc < 6; ++cc) v += s_A[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
-            v += s_B[k * 12 + t * 2] * Ubuf[2 * k] + s_B[k * 12 + t * 2 + 1] * Ubuf[2 * k + 1] + s_g[6 * k + t];
+            for (int cc = 0; cc < 6; ++cc) v += gA[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
+            v += gB[k * 12 + t * 2] * Ubuf[2 * k] + gB[k * 12 + t * 2 + 1] * Ubuf[2 * k + 1] + gg[6 * k + t];
             s_xh[6 * (k + 1) + t] = v;
         }
         __syncthreads();
@@ -838,6 +761,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void mpc_step_kernel(const K
         }
     }
     double obj = block_sum(op);
+    stamp(7, __builtin_amdgcn_s_memtime());
     const double nan = __builtin_nan("");
     double uc0 = good ? Ubuf[0] : s_up[0], uc1 = good ? Ubuf[1] : s_up[1];
     if (CLOSED) {

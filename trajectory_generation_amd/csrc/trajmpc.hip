@@ -9,7 +9,7 @@
 #include <cstring>
 
 #include "../../include/trajmpc.h"
-#include "mpc_kernel.h"
+#include "mpc_common.h"
 #include "physics.h"
 
 namespace tgmpc {
@@ -157,6 +157,8 @@ static int check_cfg(const traj_mpc_config* c) {
     return TRAJ_OK;
 }
 
+static long long* g_dbg = nullptr;  // diagnostics buffer (traj_debug_set_stamps)
+
 static inline unsigned nblk(int B, int bs) { return (unsigned)((B + bs - 1) / bs); }
 
 }  // namespace tgmpc
@@ -166,6 +168,11 @@ using namespace tgmpc;
 extern "C" {
 
 int traj_abi_version(void) { return TRAJMPC_ABI_VERSION; }
+
+int traj_debug_set_stamps(long long* buf) {
+    g_dbg = buf;
+    return TRAJ_OK;
+}
 
 const char* traj_status_string(int s) {
     switch (s) {
@@ -214,6 +221,7 @@ int traj_default_config(traj_mpc_config* c, int N, double Ts) {
     c->max_iter = 10000; c->check_interval = 25; c->scaling_iters = 10;
     c->polish = 1; c->polish_refine_iter = 3; c->adaptive_rho = 1; c->adaptive_rho_tol = 5.0;
     c->polish_mode = 0; c->polish_max_pass = 8; c->cert_tol = 1e-9; c->polish_max_rounds = 2;
+    c->warm_start = 1;
     return TRAJ_OK;
 }
 
@@ -263,31 +271,46 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
 static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                       const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
                       const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
-                      double* X_opt, double* U_opt, int* iters, int* polished, void* stream, bool lin) {
+                      double* X_opt, double* U_opt, int* iters, int* polished, void* ws, size_t ws_bytes,
+                      void* stream, bool lin) {
     if (!p || B < 0) return TRAJ_E_ARG;
     int e = check_cfg(c);
     if (e) return e;
     if (B == 0) return TRAJ_OK;
     if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
     if (!lin && (!Ad || !Bd || !g)) return TRAJ_E_ARG;
+    if (lin && (!ws || ws_bytes < traj_mpc_workspace_bytes(B, c->N))) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
     a.p = *p;
     a.c = *c;
     a.B = B;
     a.x0 = x0; a.u_prev = u_prev; a.path_ref = path_ref; a.vref = vref;
-    a.Ad = Ad; a.Bd = Bd; a.gd = g;
+    if (lin) {
+        a.wsA = (double*)ws;
+        a.wsB = a.wsA + (size_t)B * c->N * 36;
+        a.wsg = a.wsB + (size_t)B * c->N * 12;
+        a.Ad = a.wsA; a.Bd = a.wsB; a.gd = a.wsg;
+    } else {
+        a.Ad = Ad; a.Bd = Bd; a.gd = g;
+    }
     a.u_cmd = u_cmd; a.status = status; a.objective = objective; a.X_opt = X_opt; a.U_opt = U_opt;
     a.iters = iters; a.polished = polished;
+    a.dbg = g_dbg;
     return launch_mpc(a, (hipStream_t)stream, lin ? 0 : 1);
+}
+
+size_t traj_mpc_workspace_bytes(int B, int N) {
+    if (B < 0 || N < 0) return 0;
+    return ((size_t)B * (size_t)N * 54 + (size_t)B * (size_t)(6 * N + 2)) * sizeof(double);
 }
 
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                         const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
                         int* status, double* objective, double* X_opt, double* U_opt, int* iters, int* polished,
-                        void* stream) {
+                        void* workspace, size_t workspace_bytes, void* stream) {
     return mpc_common(p, c, B, x0, u_prev, path_ref, vref, nullptr, nullptr, nullptr, u_cmd, status, objective,
-                      X_opt, U_opt, iters, polished, stream, true);
+                      X_opt, U_opt, iters, polished, workspace, workspace_bytes, stream, true);
 }
 
 int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
@@ -295,7 +318,7 @@ int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, in
                       const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
                       double* X_opt, double* U_opt, int* iters, int* polished, void* stream) {
     return mpc_common(p, c, B, x0, u_prev, path_ref, vref, Ad, Bd, g, u_cmd, status, objective, X_opt, U_opt, iters,
-                      polished, stream, false);
+                      polished, nullptr, 0, stream, false);
 }
 
 static bool paths_ok(const traj_paths* ps) {
@@ -315,12 +338,14 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
 
 int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
                           double* x, double* u_prev, const double* vref, int t, int hist_T, double* hist_x,
-                          double* hist_u, int* status, int* iters, void* stream) {
+                          double* hist_u, int* status, int* iters, void* workspace, size_t workspace_bytes,
+                          void* stream) {
     if (!p || B < 0 || !paths_ok(paths)) return TRAJ_E_ARG;
     int e = check_cfg(c);
     if (e) return e;
     if (B == 0) return TRAJ_OK;
     if (!x || !u_prev || !vref) return TRAJ_E_ARG;
+    if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, c->N)) return TRAJ_E_ARG;
     if ((hist_x || hist_u) && (t < 0 || t >= hist_T)) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -337,6 +362,12 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.hist_u = hist_u;
     a.status = status;
     a.iters = iters;
+    a.dbg = g_dbg;
+    a.wsA = (double*)workspace;
+    a.wsB = a.wsA + (size_t)B * c->N * 36;
+    a.wsg = a.wsB + (size_t)B * c->N * 12;
+    a.wsWarm = a.wsg + (size_t)B * c->N * 6;
+    a.Ad = a.wsA; a.Bd = a.wsB; a.gd = a.wsg;
     return launch_mpc(a, (hipStream_t)stream, 2);
 }
 
