@@ -1,8 +1,9 @@
 """bench.py -- MPC steps/sec on B parallel spline-tracking trajectories (BASELINE.json configs[1]).
 
 One bench step = one closed-loop step of MPC/main.py:85-101 for all B trajectories of this rank
-(reference window -> mpc_step -> Euler plant), i.e. ONE launch of the fused HIP kernel
-(traj_closed_loop_step).  Inputs and state are resident in HBM for the whole timed region.
+(reference window -> mpc_step -> Euler plant) = one traj_closed_loop_step call = two HIP launches
+(linearize_kernel: rollout + FD Jacobians; solve_kernel: window, condensing, ADMM + polish, plant).
+Inputs and state are resident in HBM for the whole timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 20] [--dt 0.05]
   N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
@@ -42,7 +43,7 @@ def algorithmic_bytes_per_traj(N: int, kmax: int) -> int:
     return 8 * doubles + 4 * 4
 
 
-def cpu_baseline(w, N, Ts, ntraj, nsteps):
+def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):
     """The oracle (oracle/, C restatement of the reference path + OSQP's ADMM) on host cores."""
     import oracle as O  # test infrastructure: used here only for the CPU-baseline leg
     from trajectory_generation_amd.batch import spline_natural
@@ -54,7 +55,7 @@ def cpu_baseline(w, N, Ts, ntraj, nsteps):
         else:
             paths.append(O.Path(int(k), c))
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    cfg = O.cfg(N=N, Ts=Ts)
+    cfg = O.cfg(N=N, Ts=Ts, polish_mode=polish_mode, warm_start=warm_start)
     t0 = time.perf_counter()
     O.closed_loop_batch(paths, w["x0"][:ntraj], w["u0"][:ntraj], w["vref"], nsteps, cfg, nthreads=threads)
     dt = time.perf_counter() - t0
@@ -67,15 +68,15 @@ def cpu_baseline(w, N, Ts, ntraj, nsteps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=4096, help="trajectories per GPU")
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--dt", type=float, default=0.05)
     ap.add_argument("--kind", default="spline", choices=["spline", "mixed", "parabola"])
     ap.add_argument("--polish-mode", type=int, default=0)
-    ap.add_argument("--cpu-traj", type=int, default=1024)
-    ap.add_argument("--cpu-steps", type=int, default=4)
+    ap.add_argument("--cpu-traj", type=int, default=4096)
+    ap.add_argument("--cpu-steps", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
@@ -170,14 +171,15 @@ def main():
                    "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "mpc_step_kernel<40,true,true> (traj_closed_loop_step)",
+                     "kernel": "linearize_kernel<20,true> + solve_kernel<40,true> (one traj_closed_loop_step)",
                      "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch},
         "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
                          "iters_max": int(iters.max()),
                          "status_hist": np.bincount(stat, minlength=7).tolist()},
     }
     if not args.no_cpu and world == 1:
-        out["cpu_baseline"] = cpu_baseline(w, N, Ts, min(args.cpu_traj, B), args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(w, N, Ts, min(args.cpu_traj, B), args.cpu_steps, args.polish_mode,
+                                           cfg.warm_start)
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)

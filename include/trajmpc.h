@@ -82,8 +82,8 @@ typedef struct {
     int polish_max_pass;
     double cert_tol;
     int polish_max_rounds;
-    int warm_start;                   /* closed loop: start ADMM from the previous step's shifted
-                                       * solution (mpc_6stati.py:256 requests warm_start=True) */
+    int warm_start;                   /* closed loop: start ADMM from the previous step's adapted rho
+                                       * (mpc_6stati.py:256 requests warm_start=True) */
 } traj_mpc_config;
 
 #define TRAJ_MAX_N 40
@@ -112,8 +112,8 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
 
 /* Device workspace the MPC step needs for B instances of horizon N: the linearization A_k, B_k, g_k
  * handed from the linearize kernel to the solve kernel (B * N * 54 doubles) followed by the
- * closed-loop warm-start state (B * (6 N + 2) doubles).  Pass the same buffer to every
- * traj_closed_loop_step of one run; step t = 0 starts cold. */
+ * closed-loop warm-start state (B * 2 doubles: the previous step's rho and a valid flag).  Pass the
+ * same buffer to every traj_closed_loop_step of one run; step t = 0 starts cold. */
 size_t traj_mpc_workspace_bytes(int B, int N);
 
 /* ---- the MPC step (mpc_6stati.py:120-275) for B independent instances ----

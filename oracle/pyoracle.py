@@ -49,7 +49,7 @@ class OrcCfg(C.Structure):
         ("polish", C.c_int), ("polish_refine_iter", C.c_int), ("adaptive_rho", C.c_int),
         ("adaptive_rho_tol", C.c_double),
         ("polish_mode", C.c_int), ("polish_max_pass", C.c_int), ("cert_tol", C.c_double),
-        ("polish_max_rounds", C.c_int),
+        ("polish_max_rounds", C.c_int), ("warm_start", C.c_int),
     ]
 
 

@@ -51,6 +51,7 @@ void orc_default_cfg(orc_mpc_cfg* c, int N, double Ts) {
     c->max_iter = 10000; c->check_interval = 25; c->scaling_iters = 10;
     c->polish = 1; c->polish_refine_iter = 3; c->adaptive_rho = 1; c->adaptive_rho_tol = 5.0;
     c->polish_mode = 0; c->polish_max_pass = 8; c->cert_tol = 1e-9; c->polish_max_rounds = 2;
+    c->warm_start = 0;
 }
 
 /* ----------------------------------------------------------------- physics */
@@ -732,7 +733,7 @@ static int exact_polish(osqp_ws* w, const orc_mpc_cfg* c, double* xo, double* zo
 }
 
 /* Solve the scaled QP; returns status; x (unscaled) in xout */
-static int osqp_solve(qp_t* qp, const orc_mpc_cfg* c, double* xout, orc_info* info) {
+static int osqp_solve(qp_t* qp, const orc_mpc_cfg* c, double* xout, orc_info* info, orc_warm* warm) {
     int n = qp->n, m = qp->m;
     osqp_ws w;
     memset(&w, 0, sizeof(w));
@@ -759,6 +760,8 @@ static int osqp_solve(qp_t* qp, const orc_mpc_cfg* c, double* xout, orc_info* in
         for (int i = 0; i < m; ++i) w.E[i] = w.Einv[i] = 1.0;
         w.c = w.cinv = 1.0;
     }
+    if (warm && warm->valid)   /* start from the previous step's adapted rho (x = z = y = 0 as cold) */
+        w.rho = warm->rho < ORC_RHO_MIN ? ORC_RHO_MIN : (warm->rho > ORC_RHO_MAX ? ORC_RHO_MAX : warm->rho);
     set_rho_vec(&w);
     if (factor_kkt(w.P, w.A, w.rho_vec, n, m, c->sigma, w.K) != 0) goto done;
 
@@ -813,7 +816,9 @@ admm_loop:
     else {
         iter = c->max_iter;
         residuals(&w, c, w.x, w.z, w.y, &r);
-        if (r.prim_res <= 10.0 * r.eps_prim && r.dual_res <= 10.0 * r.eps_dual) status = ORC_OPTIMAL_INACCURATE;
+        if (rounds > 0 && r.prim_res <= r.eps_prim && r.dual_res <= r.eps_dual)
+            status = ORC_OPTIMAL;   /* exact-mode continuation ran out of iterations: eps still met */
+        else if (r.prim_res <= 10.0 * r.eps_prim && r.dual_res <= 10.0 * r.eps_dual) status = ORC_OPTIMAL_INACCURATE;
         else status = ORC_USER_LIMIT;
     }
     info->polished = 0;
@@ -863,6 +868,10 @@ done_iter:
     info->dual_res = r.dual_res;
     info->rho_final = w.rho;
     for (int j = 0; j < n; ++j) xout[j] = w.D[j] * w.x[j];
+    if (warm) {
+        warm->rho = w.rho;
+        warm->valid = (status == ORC_OPTIMAL || status == ORC_OPTIMAL_INACCURATE);
+    }
 done:
     free(w.P); free(w.q); free(w.A); free(w.l); free(w.u); free(w.D); free(w.Dinv); free(w.E); free(w.Einv);
     free(w.rho_vec); free(w.rho_inv); free(w.K);
@@ -903,6 +912,12 @@ static int all_finite(const double* v, int n) {
 int orc_mpc_step(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], const double u_prev[2],
                  const double* path_ref, const double* vref, double u_cmd[2], double* X_opt, double* U_opt,
                  orc_info* info) {
+    return orc_mpc_step_warm(p, c, x0, u_prev, path_ref, vref, u_cmd, X_opt, U_opt, info, NULL);
+}
+
+int orc_mpc_step_warm(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], const double u_prev[2],
+                      const double* path_ref, const double* vref, double u_cmd[2], double* X_opt, double* U_opt,
+                      orc_info* info, orc_warm* warm) {
     int N = c->N, n = 2 * N;
     orc_info dummy;
     if (!info) info = &dummy;
@@ -922,9 +937,10 @@ int orc_mpc_step(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], 
     } else if (qp.infeasible_const || !box_rate_feasible(c, u_prev)) {
         st = ORC_INFEASIBLE;
     } else {
-        st = osqp_solve(&qp, c, u, info);
+        st = osqp_solve(&qp, c, u, info, warm);
     }
     info->status = st;
+    if (warm && st != ORC_OPTIMAL && st != ORC_OPTIMAL_INACCURATE) warm->valid = 0;
     if (st == ORC_OPTIMAL || st == ORC_OPTIMAL_INACCURATE) {
         double* X = malloc(sizeof(double) * 6 * (N + 1));
         double* U = malloc(sizeof(double) * 2 * N);
@@ -1193,10 +1209,11 @@ void orc_closed_loop(const orc_params* p, const orc_mpc_cfg* c, const orc_path* 
     memcpy(x, x0, sizeof(x));
     memcpy(up, u0, sizeof(up));
     memcpy(traj_x, x, sizeof(x));
+    orc_warm* warm = c->warm_start ? calloc(1, sizeof(orc_warm)) : NULL;
     for (int t = 0; t < T; ++t) {
         orc_ref_window(path, x[0], N, c->Ts, vref, pref);
         orc_info info;
-        int st = orc_mpc_step(p, c, x, up, pref, vref, uc, NULL, NULL, &info);
+        int st = orc_mpc_step_warm(p, c, x, up, pref, vref, uc, NULL, NULL, &info, warm);
         if (status) status[t] = st;
         if (iters) iters[t] = info.iters;
         orc_f_cont(p, x, uc, f);
@@ -1206,6 +1223,7 @@ void orc_closed_loop(const orc_params* p, const orc_mpc_cfg* c, const orc_path* 
         traj_u[2 * t + 1] = uc[1];
         up[0] = uc[0]; up[1] = uc[1];
     }
+    free(warm);
     free(pref);
 }
 

@@ -62,6 +62,7 @@ typedef struct {
     int polish_mode, polish_max_pass;
     double cert_tol;
     int polish_max_rounds;   /* exact mode: ADMM continuation rounds (tolerance x 1e-2 each) */
+    int warm_start;          /* closed loop: start ADMM from the previous step's rho (orc_warm) */
 } orc_mpc_cfg;
 
 /* status codes (identical numbering to include/trajmpc.h) */
@@ -100,6 +101,20 @@ void orc_nominal_rollout(const orc_params* p, const double x0[6], const double u
 int orc_mpc_step(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], const double u_prev[2],
                  const double* path_ref, const double* vref, double u_cmd[2], double* X_opt, double* U_opt,
                  orc_info* info);
+
+/* Closed-loop warm start (not in the reference, whose cvxpy problem is rebuilt every call): ADMM
+ * starts from the step-size rho the previous step's solve adapted to, instead of cfg->rho.  The
+ * iterates still start at zero (shifting the previous primal/dual solution was measured to lengthen
+ * the iteration tail), and the polished optimum does not depend on rho. */
+typedef struct {
+    int valid;
+    double rho;
+} orc_warm;
+
+/* orc_mpc_step with an optional warm start (read if warm->valid, always written back). */
+int orc_mpc_step_warm(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], const double u_prev[2],
+                      const double* path_ref, const double* vref, double u_cmd[2], double* X_opt, double* U_opt,
+                      orc_info* info, orc_warm* warm);
 
 /* Batched: x0 [B,6], u_prev [B,2], path_ref [B,N+1,3], vref [B,N+1]; u_cmd [B,2], status [B],
  * objective [B], X_opt [B,6,N+1], U_opt [B,2,N], iters [B] (optional pointers may be NULL).

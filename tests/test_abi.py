@@ -1,0 +1,166 @@
+"""C-ABI boundary checks that need no GPU (include/trajmpc.h <-> libtrajmpc.so <-> ctypes).
+
+- every function include/trajmpc.h declares is exported by the built library and bound in _lib._SIGS;
+- the ctypes struct layouts equal the C compiler's (sizeof / offsetof from a gcc-compiled probe);
+- host-only entry points (defaults, strings, workspace size, argument validation) behave as documented.
+No compute entry point is launched here.
+"""
+import ctypes as C
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from trajectory_generation_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "trajmpc.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(traj_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    return _lib.lib()
+
+
+def test_every_declared_symbol_is_exported(L):
+    names = declared_functions()
+    assert len(names) >= 15
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    missing = [n for n in names if n not in exported]
+    assert not missing, f"declared in trajmpc.h but not exported: {missing}"
+    unbound = [n for n in names if n not in _lib.exported_symbols()]
+    assert not unbound, f"declared but not bound in _lib._SIGS: {unbound}"
+    extra = [n for n in _lib.exported_symbols() if n not in names]
+    assert not extra, f"bound in _lib but not declared: {extra}"
+
+
+def _c_layout(tmp_path):
+    structs = {"traj_vehicle_params": _lib.VehicleParams, "traj_mpc_config": _lib.MpcConfig,
+               "traj_paths": _lib.Paths}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {",
+             'printf("{");']
+    first = True
+    for sname, cls in structs.items():
+        items = [f'\\"sizeof\\": %zu'] + [f'\\"{f}\\": %zu' for f, _ in cls._fields_]
+        args = [f"sizeof({sname})"] + [f"offsetof({sname}, {f})" for f, _ in cls._fields_]
+        sep = "" if first else ","
+        first = False
+        lines.append(f'printf("{sep}\\"{sname}\\": {{{", ".join(items)}}}", {", ".join(args)});')
+    lines += ['printf("}\\n");', "return 0; }"]
+    c_file = tmp_path / "layout.c"
+    c_file.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-o", str(exe), str(c_file)], check=True)
+    return json.loads(subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout), structs
+
+
+def test_struct_layout_matches_c(tmp_path):
+    layout, structs = _c_layout(tmp_path)
+    for sname, cls in structs.items():
+        got = layout[sname]
+        assert got["sizeof"] == C.sizeof(cls), sname
+        for f, _ in cls._fields_:
+            assert got[f] == getattr(cls, f).offset, f"{sname}.{f}"
+
+
+def test_abi_version_and_strings(L):
+    assert L.traj_abi_version() == 1
+    for code, s in _lib.STATUS_STRINGS.items():
+        assert L.traj_status_string(code).decode() == s
+    for rc in (_lib.TRAJ_OK, _lib.TRAJ_E_ARG, _lib.TRAJ_E_UNSUPPORTED, _lib.TRAJ_E_LAUNCH):
+        assert L.traj_error_string(rc)
+
+
+def test_default_params_are_the_reference_params(L):
+    from trajectory_generation_amd.batch import REFERENCE_PARAMS
+    p = _lib.default_params()
+    for k, v in REFERENCE_PARAMS.items():
+        assert getattr(p, k) == v, k
+
+
+def test_default_config_matches_oracle(L, oracle_lib):
+    O = oracle_lib
+    for N, Ts in ((20, 0.02), (40, 0.05), (1, 0.1)):
+        c = _lib.default_config(N, Ts)
+        o = O.cfg(N=N, Ts=Ts)
+        for f, _ in _lib.MpcConfig._fields_:
+            if f == "warm_start":      # closed-loop option of the HIP path, off in the oracle by default
+                continue
+            a, b = getattr(c, f), getattr(o, f)
+            if isinstance(a, (int, float)):
+                assert a == b, f
+            else:
+                assert list(a) == list(b), f
+        # mpc_6stati.py:120-143 defaults
+        assert (c.q_c, c.q_phi, c.q_vx) == (6.0, 0.5, 0.5)
+        assert list(c.R) == [0.02, 0.0, 0.0, 2.0] and list(c.Rd) == [0.01, 0.0, 0.0, 5.0]
+        assert list(c.u_lo) == [-1.0, -0.6] and list(c.u_hi) == [1.0, 0.6]
+        assert list(c.du_lo) == [-0.5, -0.3] and list(c.du_hi) == [0.5, 0.3]
+        assert (c.eps_abs, c.eps_rel, c.max_iter, c.polish) == (1e-5, 1e-5, 10000, 1)
+
+
+def test_workspace_bytes(L):
+    for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40)):
+        assert L.traj_mpc_workspace_bytes(B, N) == (B * N * 54 + 2 * B) * 8
+    assert L.traj_mpc_workspace_bytes(-1, 20) == 0
+
+
+def test_argument_errors_are_reported_before_any_launch(L):
+    p = _lib.default_params()
+    c = _lib.default_config(20, 0.05)
+    nul = None
+    # null params / negative batch
+    assert L.traj_mpc_step_batch(None, C.byref(c), 4, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_E_ARG
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(c), -1, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_E_ARG
+    # empty batch is a no-op
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(c), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_OK
+    # horizon beyond the compiled capacity / non-positive horizon
+    for N in (0, _lib.MAX_N + 1):
+        cN = _lib.default_config(20, 0.05)
+        cN.N = N
+        assert L.traj_mpc_step_batch(C.byref(p), C.byref(cN), 0, *([nul] * 11), nul, 0, nul) in (
+            _lib.TRAJ_E_ARG, _lib.TRAJ_E_UNSUPPORTED)
+    # workspace too small (checked before launching)
+    fake = C.c_void_p(16)
+    args = [fake] * 11
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(c), 4, *args, fake, 8, nul) == _lib.TRAJ_E_ARG
+    # state bounds are not implemented on the HIP path: reported, never silently ignored
+    cx = _lib.default_config(20, 0.05)
+    cx.has_x_lo = 1
+    for i in range(6):
+        cx.x_lo[i] = -1e3
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cx), 0, *([nul] * 11), nul, 0, nul) == \
+        _lib.TRAJ_E_UNSUPPORTED
+
+
+def test_check_raises():
+    with pytest.raises(RuntimeError):
+        _lib.check(_lib.TRAJ_E_ARG, "x")
+    with pytest.raises(NotImplementedError):
+        _lib.check(_lib.TRAJ_E_UNSUPPORTED, "x")
+    _lib.check(_lib.TRAJ_OK, "x")
+
+
+def test_product_path_has_no_oracle_dependency():
+    """The shipped package must not import, call or link anything under oracle/."""
+    pkg = os.path.join(ROOT, "trajectory_generation_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")) or f == "Makefile":
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(import|from)\s+oracle\b|traj_oracle|pyoracle", src, flags=re.M), f
+    out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "traj_oracle" not in out

@@ -1,0 +1,370 @@
+"""HIP path (libtrajmpc.so through its C ABI) vs the oracle and the reference's golden vectors.
+
+Tolerances (DESIGN.md "Parity"):
+  * physics (tire_forces, f_cont, rollout, lateral_error): |gpu - ref| <= 1e-12 (1 + |ref|)
+    -- same float64 formulas; only libm ulps differ.
+  * central-difference Jacobians / A, B, g: <= 1e-8 (1 + |ref|) -- a 1-ulp difference in f is
+    divided by 2 eps = 2e-5.
+  * QP, OSQP mode (polish_mode 0) and exact mode (1) vs the oracle on the same inputs: statuses
+    identical; the polish outcome -- a residual comparison (mode 0) or a 1e-9 KKT certificate
+    (mode 1), both borderline-sensitive to roundoff -- agrees for >= 98 % / 95 % of instances and
+    the ADMM iteration count likewise; where both polished |dU| <= 1e-6 and the objective agrees to
+    1e-7 relative; where neither polished (an eps = 1e-5 ADMM point) |dU| <= 1e-4.
+  * exact mode vs the golden KKT-certified optimum: |dU| <= 1e-6 at Ts = 0.02, <= 1e-4 at
+    Ts = 0.05 (condition numbers up to 8e8).
+  * closed loop: gate (2) whole trajectories within 1e-4 at Ts = 0.02 (150 steps;
+    most within 1e-8) and for MPC/main.py's own case at Ts = 0.05 (1e-8 over 10 steps); gate (1) per-step parity along the GPU trajectory
+    for the random spline workload at Ts = 0.05, whose unstable plant amplifies 1e-12 differences
+    ~50x per step so that no two float64 implementations keep whole trajectories together.
+The QP boundary itself (cvxpy + OSQP) is not importable anywhere here: parity unpinned there,
+pinned instead to the exact optimum (golden) and to the oracle's OSQP restatement.
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests._cases import random_instances
+
+pytestmark = pytest.mark.gpu
+
+TB = pytest.importorskip("trajectory_generation_amd.batch")
+
+
+def rel(a, b):
+    return np.max(np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b))))
+
+
+@pytest.fixture(scope="module")
+def ph():
+    return np.load("tests/golden/physics.npz")
+
+
+# ------------------------------------------------------------------ physics vs reference goldens
+
+def test_tire_forces_f_cont(gpu, ph):
+    assert rel(TB.tire_forces_batch(ph["x"], ph["u"]).cpu().numpy(), ph["tire_forces"]) <= 1e-12
+    assert rel(TB.f_cont_batch(ph["x"], ph["u"]).cpu().numpy(), ph["f_cont"]) <= 1e-12
+
+
+def test_numerical_jacobian(gpu, ph):
+    Jx, Ju, f = [t.cpu().numpy() for t in TB.numerical_jacobian_batch(ph["x"], ph["u"])]
+    assert rel(Jx, ph["Jx"]) <= 1e-8
+    assert rel(Ju, ph["Ju"]) <= 1e-8
+    assert rel(f, ph["fval"]) <= 1e-12
+    # columns X, Y are exactly zero as in the reference (f does not read X, Y)
+    assert np.all(Jx[:, :, :2] == ph["Jx"][:, :, :2])
+
+
+@pytest.mark.parametrize("Ts,tag", [(0.02, "002"), (0.05, "005")])
+def test_linearize_discretize(gpu, ph, Ts, tag):
+    A, Bm, g = [t.cpu().numpy() for t in TB.linearize_discretize_batch(ph["x"], ph["u"], Ts)]
+    assert rel(A, ph["Ad_" + tag]) <= 1e-8
+    assert rel(Bm, ph["Bd_" + tag]) <= 1e-8
+    assert rel(g, ph["g_" + tag]) <= 1e-8
+
+
+def test_anchor_values(gpu):
+    an = np.load("tests/golden/anchors.npz")
+    f = TB.f_cont_batch(an["x"][None], an["u"][None]).cpu().numpy()[0]
+    np.testing.assert_allclose(f, [1, 0, 0, -0.17368083, 0.71692105, 30.66255866], atol=1e-7)
+    A, Bm, g = [t.cpu().numpy()[0] for t in TB.linearize_discretize_batch(an["x"][None], an["u"][None], 0.05)]
+    assert abs(A[5, 4] - 14.203684) < 1e-5 and abs(A[5, 5] + 1.334158) < 1e-5
+    assert abs(Bm[5, 1] - 30.010969) < 1e-5 and abs(g[3] + 0.047693) < 1e-5
+
+
+def test_lateral_error(gpu, ph):
+    a = ph["lateral_error_in"]
+    e = TB.lateral_error_batch(*[a[:, i] for i in range(5)]).cpu().numpy()
+    assert rel(e, ph["lateral_error"]) <= 1e-12
+
+
+# ------------------------------------------------------------------ full MPC step vs the oracle
+
+def _step_both(O, seed, B, N, Ts, mode, **kw):
+    x0, up, pr, vr = random_instances(seed, B, N, Ts)
+    g = TB.mpc_step_batch(x0, up, pr, vr, TB.config_struct(N=N, Ts=Ts, polish_mode=mode, **kw))
+    g = {k: v.cpu().numpy() for k, v in g.items()}
+    r = O.mpc_step_batch(x0, up, pr, vr, O.cfg(N=N, Ts=Ts, polish_mode=mode, **kw))
+    return g, r
+
+
+def _agreement(g, r, both_pol_tol, neither_tol, flag_agree, iters_equal):
+    """Statuses identical; the polish outcome (a residual comparison in OSQP mode, a KKT certificate
+    in exact mode) agrees except for borderline cases; where both polished the optimum agrees."""
+    assert np.array_equal(g["status"], r["status"])
+    ok = g["status"] <= 1
+    pg, pr = g["polished"] > 0, r["polished"] > 0
+    assert np.mean(pg == pr) >= flag_agree
+    assert np.mean(g["iters"] == r["iters"]) >= iters_equal
+    du = np.abs(g["U_opt"] - r["U_opt"]).max(axis=(1, 2))
+    both = pg & pr & ok
+    assert du[both].max(initial=0.0) <= both_pol_tol
+    neither = ~pg & ~pr & (g["status"] == 0)
+    assert du[neither].max(initial=0.0) <= neither_tol
+    dobj = np.abs(g["objective"] - r["objective"]) / np.abs(r["objective"])
+    assert dobj[both].max(initial=0.0) <= 1e-7
+    # u_cmd is U_opt[:, 0] (mpc_6stati.py:264-275)
+    assert np.array_equal(g["u_cmd"][ok], g["U_opt"][ok][:, :, 0])
+    return both
+
+
+@pytest.mark.parametrize("N,Ts,B,min_pol", [(20, 0.05, 512, 0.8), (20, 0.02, 256, 0.95), (40, 0.05, 192, 0.45),
+                                            (40, 0.02, 128, 0.8), (33, 0.02, 64, 0.8)])
+def test_mpc_step_osqp_mode_vs_oracle(gpu, oracle_lib, N, Ts, B, min_pol):
+    g, r = _step_both(oracle_lib, 11, B, N, Ts, 0)
+    both = _agreement(g, r, both_pol_tol=1e-6, neither_tol=1e-4, flag_agree=0.98, iters_equal=0.98)
+    assert both.mean() >= min_pol
+
+
+@pytest.mark.parametrize("N,Ts,B,min_cert", [(20, 0.05, 256, 0.95), (20, 0.02, 128, 0.98), (40, 0.02, 64, 0.75)])
+def test_mpc_step_exact_mode_vs_oracle(gpu, oracle_lib, N, Ts, B, min_cert):
+    g, r = _step_both(oracle_lib, 12, B, N, Ts, 1)
+    both = _agreement(g, r, both_pol_tol=1e-6, neither_tol=1e-1, flag_agree=0.95, iters_equal=0.95)
+    assert both.mean() >= min_cert
+
+
+@pytest.mark.parametrize("name", ["qp_N20_Ts005", "qp_N20_Ts002", "qp_N40_Ts005", "qp_N40_Ts002"])
+def test_qp_exact_mode_vs_golden_optimum(gpu, oracle_lib, name):
+    """QP half only (caller-supplied A, B, g from the reference) vs the golden KKT-certified optimum."""
+    gd = np.load(f"tests/golden/{name}.npz")
+    N, Ts = int(gd["N"]), float(gd["Ts"])
+    o = TB.mpc_qp_batch(gd["x0"], gd["u_prev"], gd["path_ref"], gd["vref"], gd["Ad"], gd["Bd"], gd["g"],
+                        TB.config_struct(N=N, Ts=Ts, polish_mode=1))
+    o = {k: v.cpu().numpy() for k, v in o.items()}
+    r = oracle_lib.mpc_step_batch(gd["x0"], gd["u_prev"], gd["path_ref"], gd["vref"],
+                                  oracle_lib.cfg(N=N, Ts=Ts, polish_mode=1))
+    assert np.array_equal(o["status"], r["status"]) and np.all(o["status"] <= 1)
+    cert = o["polished"] > 0
+    assert cert.mean() >= (0.9 if N == 20 else 0.35)
+    du = np.abs(o["U_opt"] - gd["U_opt"]).max(axis=(1, 2))
+    assert du[cert].max() <= (1e-6 if Ts < 0.03 else 1e-4)
+    dobj = np.abs(o["objective"] - gd["objective"]) / np.abs(gd["objective"])
+    assert dobj[cert].max() <= 1e-7
+
+
+def test_full_step_vs_golden_optimum(gpu):
+    """Full step (GPU linearization + QP) in exact mode vs the reference-linearized golden optimum."""
+    gd = np.load("tests/golden/qp_N20_Ts002.npz")
+    N, Ts = int(gd["N"]), float(gd["Ts"])
+    o = TB.mpc_step_batch(gd["x0"], gd["u_prev"], gd["path_ref"], gd["vref"],
+                          TB.config_struct(N=N, Ts=Ts, polish_mode=1))
+    o = {k: v.cpu().numpy() for k, v in o.items()}
+    cert = o["polished"] > 0
+    assert cert.mean() >= 0.9
+    du = np.abs(o["U_opt"] - gd["U_opt"]).max(axis=(1, 2))
+    assert du[cert].max() <= 1e-6
+    assert rel(o["X_opt"][cert], gd["X_opt"][cert]) <= 1e-6
+
+
+# ------------------------------------------------------------------ edge cases
+
+def test_infeasible_nonfinite_and_fallback(gpu, oracle_lib):
+    N, Ts = 20, 0.05
+    x0, up, pr, vr = random_instances(5, 6, N, Ts)
+    up[1, 0] = 3.0          # rate chain cannot reach the box: infeasible (mpc_6stati.py:197-205)
+    x0[2, 4] = np.nan       # non-finite state -> solver error
+    pr[3, 7, 1] = np.inf    # non-finite reference
+    vr[4, 2] = np.nan
+    g = TB.mpc_step_batch(x0, up, pr, vr, TB.config_struct(N=N, Ts=Ts))
+    g = {k: v.cpu().numpy() for k, v in g.items()}
+    r = oracle_lib.mpc_step_batch(x0, up, pr, vr, oracle_lib.cfg(N=N, Ts=Ts))
+    assert g["status"].tolist() == r["status"].tolist()
+    assert g["status"][1] == 3 and g["status"][2] == 6 and g["status"][3] == 6 and g["status"][4] == 6
+    for b in (1, 2, 3, 4):   # fallback: u_cmd = u_prev, no solution
+        assert np.array_equal(g["u_cmd"][b], up[b])
+        assert np.isnan(g["objective"][b]) and np.all(np.isnan(g["U_opt"][b]))
+    assert g["status"][0] <= 1 and g["status"][5] <= 1
+
+
+def test_degenerate_inputs(gpu, oracle_lib):
+    """vx = 0 and vx < 0 (the sign(vx) max(|vx|, 0.3) branch), a pinned steering box, N = 1."""
+    N, Ts = 20, 0.05
+    x0, up, pr, vr = random_instances(6, 4, N, Ts)
+    x0[0, 3] = 0.0
+    x0[1, 3] = -0.7
+    x0[2, 3] = -0.0
+    g, r = (TB.mpc_step_batch(x0, up, pr, vr, TB.config_struct(N=N, Ts=Ts)),
+            oracle_lib.mpc_step_batch(x0, up, pr, vr, oracle_lib.cfg(N=N, Ts=Ts)))
+    g = {k: v.cpu().numpy() for k, v in g.items()}
+    assert np.array_equal(g["status"], r["status"])
+    both = (g["polished"] > 0) & (r["polished"] > 0)
+    assert np.abs(g["U_opt"] - r["U_opt"]).max(axis=(1, 2))[both].max(initial=0.0) <= 1e-6
+    # equal steering bounds: delta pinned at 0 (u_prev delta within the rate reach)
+    up2 = up.copy()
+    up2[:, 1] = 0.1
+    cfgk = dict(u_bounds=((-1.0, 1.0), (0.0, 0.0)))
+    g2 = TB.mpc_step_batch(x0, up2, pr, vr, TB.config_struct(N=N, Ts=Ts, **cfgk))
+    ok = g2["status"].cpu().numpy() <= 1
+    assert ok.all()
+    assert np.abs(g2["U_opt"].cpu().numpy()[:, 1, :]).max() <= 1e-6
+    # horizon 1
+    x1, u1, p1, v1 = random_instances(7, 8, 1, Ts)
+    g1 = TB.mpc_step_batch(x1, u1, p1, v1, TB.config_struct(N=1, Ts=Ts))
+    r1 = oracle_lib.mpc_step_batch(x1, u1, p1, v1, oracle_lib.cfg(N=1, Ts=Ts))
+    assert np.array_equal(g1["status"].cpu().numpy(), r1["status"])
+    np.testing.assert_allclose(g1["U_opt"].cpu().numpy(), r1["U_opt"], atol=1e-6)
+
+
+def test_batch_composition_and_determinism(gpu):
+    """Each instance is independent of its batch neighbours and of B; repeated calls are bitwise equal."""
+    N, Ts = 20, 0.05
+    x0, up, pr, vr = random_instances(8, 300, N, Ts)
+    cfg = TB.config_struct(N=N, Ts=Ts)
+    a = TB.mpc_step_batch(x0, up, pr, vr, cfg)
+    b = TB.mpc_step_batch(x0, up, pr, vr, cfg)
+    for k in a:
+        assert torch.equal(a[k].nan_to_num(), b[k].nan_to_num()), k
+    idx = [0, 17, 299]
+    c = TB.mpc_step_batch(x0[idx], up[idx], pr[idx], vr[idx], cfg)
+    for k in ("u_cmd", "U_opt", "status", "iters"):
+        assert torch.equal(a[k][idx].nan_to_num(), c[k].nan_to_num()), k
+    e = TB.mpc_step_batch(x0[:0], up[:0], pr[:0], vr[:0], cfg)
+    assert e["u_cmd"].shape == (0, 2)
+
+
+# ------------------------------------------------------------------ closed loop (MPC/main.py)
+
+def _oracle_paths(O, w):
+    from trajectory_generation_amd.batch import spline_natural
+    out = []
+    for k, c, kn in zip(w["kinds"], w["pcs"], w["knots"]):
+        if k == 2:
+            out.append(O.Path(2, (0, 0, 0, 0), xk=kn[0], coef=spline_natural(kn[0], kn[1]).reshape(-1)))
+        else:
+            out.append(O.Path(int(k), c))
+    return out
+
+
+def test_ref_window_vs_oracle(gpu, oracle_lib):
+    from trajectory_generation_amd.workload import make_workload
+    for kind in ("spline", "mixed"):
+        w = make_workload(32, 20, 0.05, kind=kind, seed=4)
+        paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+        xs = w["x0"][:, 0] + np.linspace(-10, 40, 32)       # also outside the knots (extrapolation)
+        g = TB.ref_window_batch(paths, xs, np.tile(w["vref"], (32, 1)), 20, 0.05).cpu().numpy()
+        ops = _oracle_paths(oracle_lib, w)
+        r = np.stack([oracle_lib.ref_window(p, x, 20, 0.05, w["vref"]) for p, x in zip(ops, xs)])
+        assert rel(g, r) <= 1e-12
+
+
+def _closed_loop_both(O, kind, N, Ts, T, warm, B, seed=9, mode=0):
+    from trajectory_generation_amd.workload import make_workload
+    w = make_workload(B, N, Ts, kind=kind, seed=seed)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=warm, polish_mode=mode)
+    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg)
+    res = {k: v.cpu().numpy() for k, v in res.items()}
+    r = O.closed_loop_batch(_oracle_paths(O, w), w["x0"], w["u0"], w["vref"], T,
+                            O.cfg(N=N, Ts=Ts, warm_start=warm, polish_mode=mode))
+    return w, paths, cfg, res, r
+
+
+@pytest.mark.parametrize("kind,N,Ts,T,warm", [("mixed", 20, 0.02, 150, 0), ("mixed", 20, 0.02, 150, 1),
+                                              ("spline", 40, 0.02, 60, 1)])
+def test_closed_loop_trajectories_vs_oracle(gpu, oracle_lib, kind, N, Ts, T, warm):
+    """SURVEY.md 8(d) gate (2): whole closed-loop trajectories agree in the stable regime (Ts = 0.02)."""
+    w, _, _, res, r = _closed_loop_both(oracle_lib, kind, N, Ts, T, warm, B=16)
+    assert np.array_equal(res["status"].T, r["status"])
+    err = np.abs(res["X"] - r["X"]).max(axis=2)          # [B, T+1]
+    # a borderline polish flip moves one step's u by <= 1e-4; the stable plant then contracts it
+    assert err.max() <= 1e-4, err.max(axis=0)
+    assert np.mean(err.max(axis=1) <= 1e-8) >= 0.75
+    assert np.mean(res["iters"].T == r["iters"]) >= 0.95
+
+
+def test_closed_loop_main_py_case_vs_oracle(gpu, oracle_lib):
+    """MPC/main.py itself (parabola y = 0.1 x^2, x0 = [0, .5, 0, 1, 0, 0], Ts = 0.05): 20 steps agree."""
+    _, _, _, res, r = _closed_loop_both(oracle_lib, "parabola", 20, 0.05, 20, 1, B=2)
+    assert np.array_equal(res["status"].T, r["status"])
+    err = np.abs(res["X"] - r["X"]).max(axis=(0, 2))
+    # 1e-12 at step 1, growing ~2x per step through the unstable lateral mode
+    assert err[:10].max() <= 1e-8 and err.max() <= 1e-4, err
+
+
+@pytest.mark.parametrize("warm", [0, 1])
+def test_closed_loop_per_step_parity_ts005(gpu, oracle_lib, warm):
+    """SURVEY.md 8(d) gate (1) at Ts = 0.05, where the plant is unstable (rho(A) up to 6.45) and
+    1e-12 differences grow ~50x per step: every step of the GPU closed loop is re-solved by the
+    oracle from the GPU's own state and must agree (statuses identical; u_cmd as in the step tests)."""
+    N, Ts, T, B = 20, 0.05, 20, 48
+    w, paths, cfg, res, _ = _closed_loop_both(oracle_lib, "spline", N, Ts, T, warm, B)
+    vr = np.tile(w["vref"], (B, 1))
+    n_same_pol = n = 0
+    for t in range(T):
+        xt = res["X"][:, t]
+        ut = res["U"][:, t - 1] if t > 0 else w["u0"]
+        prt = TB.ref_window_batch(paths, xt[:, 0], vr, N, Ts).cpu().numpy()
+        g = {k: v.cpu().numpy() for k, v in TB.mpc_step_batch(xt, ut, prt, vr, cfg).items()}
+        # the closed-loop kernel applied exactly what the step entry point returns (warm start off)
+        if not warm:
+            assert np.array_equal(g["u_cmd"], res["U"][:, t])
+            assert np.array_equal(g["status"], res["status"][t])
+        ro = oracle_lib.mpc_step_batch(xt, ut, prt, vr, oracle_lib.cfg(N=N, Ts=Ts))
+        assert np.array_equal(g["status"], ro["status"])
+        same = (g["polished"] > 0) == (ro["polished"] > 0)
+        du = np.abs(g["u_cmd"] - ro["u_cmd"]).max(axis=1)
+        assert du[same].max() <= 1e-4
+        n_same_pol += same.sum()
+        n += B
+    assert n_same_pol / n >= 0.98
+
+
+def test_closed_loop_history_matches_single_steps(gpu):
+    """run_closed_loop's device histories equal step-by-step calls of the per-step entry point."""
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B = 20, 0.05, 5, 16
+    w = make_workload(B, N, Ts, kind="spline", seed=2)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=0)
+    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg)
+    x = np.array(w["x0"])
+    u = np.array(w["u0"])
+    for t in range(T):
+        pr = TB.ref_window_batch(paths, x[:, 0], np.tile(w["vref"], (B, 1)), N, Ts)
+        o = TB.mpc_step_batch(x, u, pr, np.tile(w["vref"], (B, 1)), cfg)
+        uc = o["u_cmd"].cpu().numpy()
+        f = TB.f_cont_batch(x, uc).cpu().numpy()
+        x = x + Ts * f
+        u = uc
+        assert np.array_equal(res["U"].cpu().numpy()[:, t], uc)
+        assert np.array_equal(res["X"].cpu().numpy()[:, t + 1], x)
+
+
+# ------------------------------------------------------------------ drop-in module
+
+def test_dropin_mpc_step_contract(gpu, oracle_lib):
+    from trajectory_generation_amd import mpc_6stati as M
+    x0, up, pr, vr = random_instances(13, 1, 20, 0.05)
+    u, status, info = M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, vref=vr[0])
+    assert status in ("optimal", "optimal_inaccurate")
+    assert isinstance(u, np.ndarray) and u.shape == (2,)
+    assert set(info) == {"status", "objective", "X_opt", "U_opt", "path_ref", "vref"}
+    assert info["X_opt"].shape == (6, 21) and info["U_opt"].shape == (2, 20)
+    np.testing.assert_array_equal(info["X_opt"][:, 0], x0[0])
+    r = oracle_lib.mpc_step(x0[0], up[0], pr[0], vr[0], oracle_lib.cfg(N=20, Ts=0.05))
+    np.testing.assert_allclose(u, r["u_cmd"], atol=1e-6)
+    # vref None -> x0[3]; scalar vref
+    _, s2, i2 = M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20)
+    assert np.all(i2["vref"] == x0[0, 3])
+    _, s3, i3 = M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, vref=1.5)
+    assert np.all(i3["vref"] == 1.5)
+    # bad path_ref shape -> AssertionError (mpc_6stati.py:151)
+    with pytest.raises(AssertionError):
+        M.mpc_step(x0[0], up[0], pr[0][:-1], Ts=0.05, N=20)
+    # infeasible -> (u_prev, status, {})
+    u4, s4, i4 = M.mpc_step(x0[0], [3.0, 0.0], pr[0], Ts=0.05, N=20)
+    assert s4 == "infeasible" and i4 == {} and np.array_equal(u4, [3.0, 0.0])
+    # non-PSD weight -> cvxpy DCPError inside the reference's try
+    u5, s5, i5 = M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, R=np.diag([-1.0, 1.0]))
+    assert s5 == "Solver Error: DCPError" and i5 == {}
+    # params override (dict copy, :144-146)
+    _, s6, i6 = M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, params={"m": 0.05})
+    assert s6 in ("optimal", "optimal_inaccurate")
+    assert not np.array_equal(i6["U_opt"], info["U_opt"])
+
+
+def test_state_bounds_fail_loudly(gpu):
+    from trajectory_generation_amd import mpc_6stati as M
+    x0, up, pr, vr = random_instances(14, 1, 20, 0.05)
+    with pytest.raises(NotImplementedError):
+        M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, x_lo=[-1e3] * 6)

@@ -69,7 +69,7 @@ struct KArgs {
     double* wsA;             // linearization outputs (workspace): [B,N,6,6], [B,N,6,2], [B,N,6]
     double* wsB;
     double* wsg;
-    double* wsWarm;          // closed loop: per instance [U (2N), y_box (2N), y_rate (2N), rho, valid]
+    double* wsWarm;          // closed loop: per instance [rho, valid] of the previous step
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

@@ -452,28 +452,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
         int phase = PH_ADMM;
         double rho = c.rho;
         double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
-        // Warm start (closed loop, t > 0): the previous step's solution shifted one stage
-        // (receding horizon), mapped into this step's scaling.  mpc_6stati.py:256 asks OSQP for
-        // warm_start=True, which is a no-op there because a new Problem is built every call; the
-        // polished optimum does not depend on the starting point.
+        // Warm start (closed loop, t > 0): start from the rho the previous step's solve adapted to
+        // (iterates start at zero as cold; shifting the previous primal/dual point was measured to
+        // lengthen the iteration tail).  mpc_6stati.py:256 asks OSQP for warm_start=True, a no-op
+        // there because a new Problem is built every call; the polished optimum does not depend on rho.
         if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {
-            const double* wv = a.wsWarm + (size_t)b * (6 * N + 2);
-            if (wv[6 * N + 1] != 0.0) {
-                rho = fmin(fmax(wv[6 * N], RHO_MIN), RHO_MAX);
-                const int src = (kk < N - 1) ? t + 2 : t;          // shift one stage
-                const int srcm = (kk < N - 1) ? t : t - 2;         // previous variable of the rate row
-                if (own) {
-                    const double D = cold(C_D), Eb = cold(C_EB), Er = cold(C_ER);
-                    const double U = wv[src];
-                    const double Um = (kk == 0) ? s_up[ch] : wv[srcm];
-                    x = U / D;
-                    zb = clampd(Eb * U, slb, sub);
-                    zr = clampd(Er * (U - Um), slr, sur);
-                    const double yscale = cs;                      // y_scaled = c y / E
-                    yb = (kk < N - 1) ? yscale * wv[2 * N + src] / Eb : 0.0;
-                    yr = (kk < N - 1) ? yscale * wv[4 * N + src] / Er : 0.0;
-                }
-            }
+            const double* wv = a.wsWarm + 2 * (size_t)b;
+            if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
         }
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
         Res r = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -594,8 +579,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
                 else {
                     iter = c.max_iter;
                     r = residuals(x, zb, zr, yb, yr);
-                    status = (r.pr <= 10.0 * r.eps_p && r.dr <= 10.0 * r.eps_d) ? TRAJ_STATUS_OPTIMAL_INACCURATE
-                                                                                  : TRAJ_STATUS_USER_LIMIT;
+                    // an exact-mode continuation round that runs out of iterations still meets eps
+                    status = (rounds > 0 && r.pr <= r.eps_p && r.dr <= r.eps_d) ? TRAJ_STATUS_OPTIMAL
+                             : (r.pr <= 10.0 * r.eps_p && r.dr <= 10.0 * r.eps_d) ? TRAJ_STATUS_OPTIMAL_INACCURATE
+                                                                                 : TRAJ_STATUS_USER_LIMIT;
                 }
                 if (status == TRAJ_STATUS_OPTIMAL && c.polish) {
                     // OSQP active sets: lower if z - l < -y, upper if u - z < y
@@ -703,24 +690,17 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
         }
         if (iter > c.max_iter) iter = c.max_iter;
         xsol = cold(C_D) * x;
-        if (CLOSED && a.wsWarm) {
-            double* wv = a.wsWarm + (size_t)b * (6 * N + 2);
+        if (CLOSED && a.wsWarm && t == 0) {
             const bool okst = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
-            if (own) {
-                wv[t] = xsol;
-                wv[2 * N + t] = yb * cold(C_EB) * csinv;   // unscaled y = E y / c
-                wv[4 * N + t] = yr * cold(C_ER) * csinv;
-            }
-            if (t == 0) {
-                wv[6 * N] = rho;
-                wv[6 * N + 1] = okst ? 1.0 : 0.0;
-            }
+            a.wsWarm[2 * (size_t)b] = rho;
+            a.wsWarm[2 * (size_t)b + 1] = okst ? 1.0 : 0.0;
         }
         stamp(8, nfact);
         stamp(10, ps);
     } else {
         status = early;
         iter = 0;
+        if (CLOSED && a.wsWarm && t == 0) a.wsWarm[2 * (size_t)b + 1] = 0.0;
     }
 
     stamp(6, __builtin_amdgcn_s_memtime());

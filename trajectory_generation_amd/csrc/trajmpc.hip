@@ -302,7 +302,7 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
     if (B < 0 || N < 0) return 0;
-    return ((size_t)B * (size_t)N * 54 + (size_t)B * (size_t)(6 * N + 2)) * sizeof(double);
+    return ((size_t)B * (size_t)N * 54 + (size_t)B * 2) * sizeof(double);
 }
 
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
