@@ -165,7 +165,8 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
 /* ---- diagnostics ----
  * Subsequent MPC launches write, per instance b, 16 int64 slots at buf[16 b ..] (device memory):
  * [0..7] s_memtime at phase boundaries (start, inputs, rollout, linearization, condensing,
- * scaling, solver end, outputs), [8] KKT factorizations, [9] ADMM iterations, [10] polish passes.
+ * scaling, solver end, outputs), [8] KKT factorizations, [9] ADMM iterations, [10] polish passes,
+ * [11] cycles in residual checks, [12] cycles in factorizations, [13] cycles in polish, [14] checks.
  * NULL disables.  For profiling only; never enabled by the product path. */
 int traj_debug_set_stamps(long long* buf);
 

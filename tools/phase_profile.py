@@ -21,8 +21,9 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     torch.cuda.synchronize()
     _lib.lib().traj_debug_set_stamps(None)
     d = dbg.cpu().numpy()
-    names = ["inputs", "rollout", "linearize", "condense", "scale", "solve", "outputs"]
-    ph = np.diff(d[:, :8], axis=1)
+    names = ["inputs", "condense", "scale", "solve", "outputs"]
+    idx = [0, 1, 4, 5, 6, 7]
+    ph = np.diff(d[:, idx], axis=1)
     print(f"kernel {e0.elapsed_time(e1):.3f} ms  B={B} N={N} kind={kind} polish_mode={polish_mode}")
     print("phase       median      p90       max   (cycles)")
     for i, nm in enumerate(names):
@@ -31,12 +32,25 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     print(f"{'total':10s} {np.median(tot):9.0f} {np.percentile(tot, 90):9.0f} {tot.max():9.0f}")
     it, nf, ps = d[:, 9], d[:, 8], d[:, 10]
     print("iters median", np.median(it), "p99", np.percentile(it, 99), "max", it.max(), " factorizations median", np.median(nf), "max", nf.max())
-    solve = ph[:, 5]
+    solve = ph[:, 3]
     A = np.stack([it, nf, np.ones_like(it)], 1).astype(float)
     coef, *_ = np.linalg.lstsq(A, solve.astype(float), rcond=None)
     print("solve cycles ~ %.0f/iter + %.0f/factorization + %.0f" % tuple(coef))
-    span = (d[:, 7].max() - d[:, 0].min())
-    print("first start -> last end: %.0f cycles; start spread %.0f" % (span, d[:, 0].max() - d[:, 0].min()))
+    res, sw, pol, nres = d[:, 11], d[:, 12], d[:, 13], d[:, 14]
+    admm = solve - res - sw - pol
+    print("solve split (median / sum share): residual checks %.0f / %.2f, sweeps %.0f / %.2f, polish %.0f / %.2f, ADMM iterations %.0f / %.2f"
+          % (np.median(res), res.sum() / solve.sum(), np.median(sw), sw.sum() / solve.sum(), np.median(pol), pol.sum() / solve.sum(),
+             np.median(admm), admm.sum() / solve.sum()))
+    print("per residual check %.0f cycles, per sweep %.0f, per plain iteration %.0f"
+          % (res.sum() / max(nres.sum(), 1), sw.sum() / max(nf.sum(), 1), admm.sum() / max(it.sum(), 1)))
+    rs, re = d[:, 2] - d[:, 2].min(), d[:, 3] - d[:, 2].min()      # 100 MHz ticks
+    print("wall (us): kernel span %.1f; starts: median %.1f max %.1f; ends: median %.1f p99 %.1f max %.1f"
+          % (re.max() / 100, np.median(rs) / 100, rs.max() / 100, np.median(re) / 100, np.percentile(re, 99) / 100, re.max() / 100))
+    last = np.argsort(re)[-5:]
+    for b in last:
+        print("  late finisher b=%d start %.1f us end %.1f us iters %d cycles %d" % (b, rs[b] / 100, re[b] / 100, it[b], tot[b]))
+    clk = 0.1 * tot / np.maximum(re - rs, 1)
+    print("in-kernel clock (median over instances): %.2f GHz" % np.median(clk))
 
 if __name__ == "__main__":
     main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0)

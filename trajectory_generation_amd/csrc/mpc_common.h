@@ -140,5 +140,64 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// 1/d for a normal, finite d: v_rcp_f64 + two Newton steps (the IEEE division sequence without its
+// scale / fix-up steps; within an ulp of 1.0 / d)
+__device__ __forceinline__ double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    r = fma(fma(-d, r, 1.0), r, r);
+    return r;
+}
+
+// ---- DPP cross-lane moves (gfx9 data-parallel primitives: VALU, no LDS traffic) -------------
+// CTRL: 0x130 wave_shl:1 (lane t receives lane t+1), 0x138 wave_shr:1 (lane t-1), 0xB1 / 0x4E
+// quad_perm [1,0,3,2] / [2,3,0,1], 0x141 row_half_mirror, 0x140 row_mirror, 0x142 row_bcast:15,
+// 0x143 row_bcast:31.  Lanes whose source is outside the wave, or whose row is masked off, get 0.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double v) {
+    int lo = __double2loint(v), hi = __double2hiint(v);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROW_MASK, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROW_MASK, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_up2(double v) { return dpp_d<0x130>(dpp_d<0x130>(v)); }  // lane t+2
+__device__ __forceinline__ double lane_dn2(double v) { return dpp_d<0x138>(dpp_d<0x138>(v)); }  // lane t-2
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// Wave-wide max of V non-negative values (NaN if any lane holds a NaN), uniform result.
+// Butterfly inside rows of 16 lanes, then row_bcast 15 / 31 into lane 63, then readlane.
+template <int V>
+__device__ __forceinline__ void wave_max_dpp(double (&v)[V]) {
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const bool nan = __ballot(v[i] != v[i]) != 0;
+        double m = v[i];
+        m = fmax(m, dpp_d<0xB1>(m));
+        m = fmax(m, dpp_d<0x4E>(m));
+        m = fmax(m, dpp_d<0x141>(m));
+        m = fmax(m, dpp_d<0x140>(m));
+        m = fmax(m, dpp_d<0x142, 0xa>(m));
+        m = fmax(m, dpp_d<0x143, 0xc>(m));
+        m = readlane_d(m, 63);
+        v[i] = nan ? __builtin_nan("") : m;
+    }
+}
+
+// Wave-wide sum, uniform result (same DPP pattern).
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v += dpp_d<0xB1>(v);
+    v += dpp_d<0x4E>(v);
+    v += dpp_d<0x141>(v);
+    v += dpp_d<0x140>(v);
+    v += dpp_d<0x142, 0xa>(v);
+    v += dpp_d<0x143, 0xc>(v);
+    return readlane_d(v, 63);
+}
+
 
 }  // namespace tgmpc

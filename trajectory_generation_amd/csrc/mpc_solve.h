@@ -34,12 +34,17 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     __shared__ double s_pref[3 * (NM + 1)];
     __shared__ double s_vref[NM + 1];
     __shared__ double s_x0[6], s_up[2];
-    __shared__ double s_P[NP];          // scaled P, packed upper triangle (row-major)
-    __shared__ double s_cold[8 * NT];   // per-lane values used only off the ADMM hot path
+    // one region, two lives: A_k, B_k, g_k of every stage staged for the condensing, then (once P
+    // is formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values
+    constexpr int NLIN = 54 * NM;
+    constexpr int NBIG = (NP + 8 * NT > NLIN) ? NP + 8 * NT : NLIN;
+    __shared__ __attribute__((aligned(16))) double s_big[NBIG];
+    double* const s_P = s_big;
+    double* const s_cold = s_big + NP;
     __shared__ double s_xh[(NM + 1) * 6];
     __shared__ double s_sc[(NM + 1) * 2];
-    __shared__ double s_e[(NM + 1) * 3];
-    __shared__ double s_ex[6 * NN];     // exchange / broadcast buffers (rotating)
+    __shared__ __attribute__((aligned(16))) double s_ex[6 * NN];   // exchange / broadcast buffers
+    __shared__ __attribute__((aligned(16))) double s_sw[2 * (2 * NN + 2)];   // sweep pivot columns
     __shared__ double s_red[16 * WAVES];
     __shared__ int s_flag[4];
 
@@ -60,12 +65,19 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
 
     // ---- block helpers -------------------------------------------------------------
     auto exch = [&](double v, int delta) -> double {   // value of variable t+delta (0 outside)
-        double* buf = s_ex + (xb & 3) * NN;
-        xb++;
-        if (own) buf[t] = v;
-        __syncthreads();
-        int s = t + delta;
-        return (own && s >= 0 && s < n) ? buf[s] : 0.0;
+        if constexpr (WAVES == 1) {
+            // delta is +-2 at every call site: two DPP wave shifts, no LDS round trip
+            const double vm = own ? v : 0.0;
+            const double r = (delta > 0) ? lane_up2(vm) : lane_dn2(vm);
+            return own ? r : 0.0;
+        } else {
+            double* buf = s_ex + (xb & 3) * NN;
+            xb++;
+            if (own) buf[t] = v;
+            __syncthreads();
+            int s = t + delta;
+            return (own && s >= 0 && s < n) ? buf[s] : 0.0;
+        }
     };
     auto bcast = [&](double v) -> double* {            // publish v_t for all, returns buffer
         double* buf = s_ex + (xb & 3) * NN;
@@ -76,10 +88,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     };
     auto block_max = [&](auto& v) {                   // in-place max over the block (uniform result)
         constexpr int V = sizeof(v) / sizeof(double);
-        wave_max<V>(v);
-        if (WAVES == 1)
-            for (int i = 0; i < V; ++i) v[i] = uniformize(v[i]);
-        if (WAVES > 1) {
+        if (WAVES == 1) {
+            wave_max_dpp<V>(v);
+        } else {
+            wave_max<V>(v);
             if (lane == 0)
                 for (int i = 0; i < V; ++i) s_red[wid * V + i] = v[i];
             __syncthreads();
@@ -92,9 +104,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
         }
     };
     auto block_sum = [&](double v) -> double {
-        v = wave_sum(v);
-        if (WAVES == 1) v = uniformize(v);
-        if (WAVES > 1) {
+        if (WAVES == 1) {
+            v = wave_sum_dpp(v);
+        } else {
+            v = wave_sum(v);
             if (lane == 0) s_red[wid] = v;
             __syncthreads();
             double s = 0.0;
@@ -153,75 +166,86 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     const double* gA = a.Ad + (size_t)b * N * 36;   // this instance's linearization
     const double* gB = a.Bd + (size_t)b * N * 12;
     const double* gg = a.gd + (size_t)b * N * 6;
-    stamp(2, __builtin_amdgcn_s_memtime());
-    stamp(3, __builtin_amdgcn_s_memtime());
+    stamp(2, __builtin_amdgcn_s_memrealtime());   // 100 MHz wall clock (comparable across XCDs)
     // ---- 3. condensed QP (:180-250) --------------------------------------------------
-    // free response xh_{k+1} = A_k xh_k + g_k
-    if (t < 6) s_xh[t] = s_x0[t];
-    __syncthreads();
-    for (int k = 0; k < N; ++k) {
-        if (t < 6) {
-            double v = 0.0;
-            for (int cc = 0; cc < 6; ++cc) v += gA[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
-            s_xh[6 * (k + 1) + t] = v + gg[6 * k + t];
-        }
-        __syncthreads();
+    // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
+    {
+        for (int i = t; i < 36 * N; i += NT) s_big[i] = gA[i];
+        for (int i = t; i < 12 * N; i += NT) s_big[36 * N + i] = gB[i];
+        for (int i = t; i < 6 * N; i += NT) s_big[48 * N + i] = gg[i];
     }
-    // per stage: sin/cos(phi*), tracking errors e_k of the free response, constant cost
-    const double W0 = c.q_c, W1 = c.q_phi, W2 = c.q_vx;
+    const double* const cA = s_big;
+    const double* const cB = s_big + 36 * N;
+    const double* const cg = s_big + 48 * N;
+    // sin / cos of phi*_k for every stage (lane-parallel)
     for (int k = t; k <= N; k += NT) {
-        double Pr = s_pref[3 * k + 2], s, co;
-        sincos(Pr, &s, &co);
-        s_sc[2 * k] = s;
-        s_sc[2 * k + 1] = co;
-        const double* xk = s_xh + 6 * k;
-        double e0 = s * (xk[0] - s_pref[3 * k]) - co * (xk[1] - s_pref[3 * k + 1]);
-        double e1 = xk[2] - Pr;
-        double e2 = xk[3] - s_vref[k];
-        s_e[3 * k] = e0;
-        s_e[3 * k + 1] = e1;
-        s_e[3 * k + 2] = e2;
+        double sk, ck;
+        sincos(s_pref[3 * k + 2], &sk, &ck);
+        s_sc[2 * k] = sk;
+        s_sc[2 * k + 1] = ck;
     }
     __syncthreads();
 
+    // P = sum_k G_k' C_k' 2W C_k G_k and q = sum_k G_k' C_k' 2W e_k, accumulated stage by stage:
+    // lane t carries column t of the input sensitivity G_k (6-vector); the free response xh_k and
+    // its tracking errors e_k are uniform and computed by every lane.  With the weights split as
+    // sqrt(2W) into F = sqrt(2W) C G, each stage adds F_t F_j (3 FMAs per entry) -- a product that is
+    // commutative, so P stays bitwise symmetric.
     double Prow[NN];
 #pragma unroll
     for (int j = 0; j < NN; ++j) Prow[j] = 0.0;
     double qi = 0.0;
     {
-        // sensitivity column j = t of G_k (6-vector), propagated forward; P accumulated row-wise
-        double G[6] = {0, 0, 0, 0, 0, 0};
+        const double sw0 = sqrt(2.0 * c.q_c), sw1 = sqrt(2.0 * c.q_phi), sw2 = sqrt(2.0 * c.q_vx);
+        double xh[6], G[6] = {0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < 6; ++i) xh[i] = s_x0[i];
         for (int k = 0; k < N; ++k) {
+            const double* Ak = cA + 36 * k;
+            // free response xh_{k+1} = A_k xh_k + g_k (uniform)
+            double xn[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                double v = cg[6 * k + r];
+#pragma unroll
+                for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], xh[cc], v);
+                xn[r] = v;
+            }
+#pragma unroll
+            for (int r = 0; r < 6; ++r) xh[r] = xn[r];
+            // input sensitivities: columns of inputs applied before stage k propagate, stage k's
+            // inputs enter through B_k
             if (own) {
                 if (t < 2 * k) {
                     double Gn[6];
+#pragma unroll
                     for (int r = 0; r < 6; ++r) {
                         double v = 0.0;
-                        for (int cc = 0; cc < 6; ++cc) v = fma(gA[k * 36 + r * 6 + cc], G[cc], v);
+#pragma unroll
+                        for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], G[cc], v);
                         Gn[r] = v;
                     }
+#pragma unroll
                     for (int r = 0; r < 6; ++r) G[r] = Gn[r];
                 } else if (kk == k) {
-                    for (int r = 0; r < 6; ++r) G[r] = gB[k * 12 + r * 2 + ch];
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) G[r] = cB[12 * k + 2 * r + ch];
                 }
             }
-            // output sensitivities of stage k+1: F = C_{k+1} G
-            const double s = s_sc[2 * (k + 1)], co = s_sc[2 * (k + 1) + 1];
-            double F0 = s * G[0] - co * G[1], F1 = G[2], F2 = G[3];
+            // stage k+1 outputs: tracking errors of the free response, weighted sensitivities
+            const int k1 = k + 1;
+            const double sk = s_sc[2 * k1], ck = s_sc[2 * k1 + 1];
+            const double e0 = sk * (xh[0] - s_pref[3 * k1]) - ck * (xh[1] - s_pref[3 * k1 + 1]);
+            const double e1 = xh[2] - s_pref[3 * k1 + 2];
+            const double e2 = xh[3] - s_vref[k1];
+            const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
+            qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
             double* buf = s_ex + (xb & 1) * 3 * NN;   // 2 rotating slots of 3*NN
             xb++;
             if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
             __syncthreads();
-            {
-                // P_tj += 2 W (F_t F_j): the product F_t F_j is symmetric in (t, j), so P stays
-                // bitwise symmetric; entries j >= n read the zero padding
-                const double w0 = 2.0 * W0, w1 = 2.0 * W1, w2 = 2.0 * W2;
-                const double* ek = s_e + 3 * (k + 1);
-                qi += w0 * F0 * ek[0] + w1 * F1 * ek[1] + w2 * F2 * ek[2];
 #pragma unroll
-                for (int j = 0; j < NN; ++j)
-                    Prow[j] = fma(w0, F0 * buf[j], fma(w1, F1 * buf[NN + j], fma(w2, F2 * buf[2 * NN + j], Prow[j])));
-            }
+            for (int j = 0; j < NN; ++j)
+                Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
         }
         __syncthreads();
     }
@@ -372,29 +396,18 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
         auto Pmul = [&](double v) -> double {  // (P v)_t  (rows >= n are zero)
             double* vb = bcast(v);
             const int tt = opaque_t();
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < NN; j += 4) {
-                s0 = fma(s_P[paddr(j, tt)], vb[j], s0);
-                if (j + 1 < NN) s1 = fma(s_P[paddr(j + 1, tt)], vb[j + 1], s1);
-                if (j + 2 < NN) s2 = fma(s_P[paddr(j + 2, tt)], vb[j + 2], s2);
-                if (j + 3 < NN) s3 = fma(s_P[paddr(j + 3, tt)], vb[j + 3], s3);
-            }
-            return own ? (s0 + s1) + (s2 + s3) : 0.0;
+            for (int j = 0; j < NN; ++j) sa[j & 7] = fma(s_P[paddr(j, tt)], vb[j], sa[j & 7]);
+            return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
         };
         double Krow[NN];
         auto Kmul = [&](double v) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
             double* vb = bcast(v);
-            double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+            double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < NN; j += 4) {
-                s0 = fma(Krow[j], vb[j], s0);
-                if (j + 1 < NN) s1 = fma(Krow[j + 1], vb[j + 1], s1);
-                if (j + 2 < NN) s2 = fma(Krow[j + 2], vb[j + 2], s2);
-                if (j + 3 < NN) s3 = fma(Krow[j + 3], vb[j + 3], s3);
-                if ((j & 7) == 4) __builtin_amdgcn_sched_barrier(0);   // bound live LDS values
-            }
-            return own ? (s0 + s1) + (s2 + s3) : 0.0;
+            for (int j = 0; j < NN; ++j) sa[j & 7] = fma(Krow[j], vb[j], sa[j & 7]);
+            return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
         };
         auto rho_for = [&](double l, double u, double rho) -> double {
             if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
@@ -467,7 +480,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
         const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
         iter = 1;
         int nfact = 0;
+        // diagnostics (traj_debug_set_stamps): cycles in residual checks / sweeps / polish
+        const bool prof = a.dbg != nullptr;
+        long long cyc_res = 0, cyc_sweep = 0, cyc_pol = 0, n_res = 0, t_mark = 0;
+        bool pol_open = false;
+        auto tic = [&]() { if (prof) t_mark = __builtin_amdgcn_s_memtime(); };
+        auto toc = [&](long long& acc) { if (prof) acc += __builtin_amdgcn_s_memtime() - t_mark; };
         while (phase != PH_DONE) {
+            if (pol_open) { toc(cyc_pol); pol_open = false; }
             ++nfact;
             // ---- build K (row t) ----
             const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
@@ -495,30 +515,59 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
             // so the pivot row in rotated order is the contiguous slice cb[pv .. pv + NN)
             // (K symmetric: K[pv][c] = K[c][pv]).  Padding pivots (>= n) are identity and exact.
             bool ok = true;
-#pragma nounroll
-            for (int pv = 0; pv < NN; ++pv) {
-                double* cb = s_ex + (pv & 1) * 2 * NN;
+            tic();
+            {
+                // Pivot pv: K_tj <- K_tj - (K_tp / d) K_pj off the pivot row, K_pj / d on it, column
+                // pv <- K_tp / d (and -1/d on the pivot).  The next pivot's column (new Krow[0]) is
+                // computed and published FIRST, so its LDS write overlaps the remaining FMAs.
+                // Buffers: column published twice (s_sw[o + t], s_sw[o + t + NN]) with o = pv & 1, so
+                // the rotated pivot row s_sw + o + pv starts 16-byte aligned.
+                constexpr int SB = 2 * NN + 2;
                 if (t < NN) {
-                    cb[t] = Krow[0];
-                    cb[t + NN] = Krow[0];
+                    s_sw[t] = Krow[0];
+                    s_sw[t + NN] = Krow[0];
                 }
-                __syncthreads();
-                const double* prow = cb + pv;
-                const double d = prow[0];
-                ok = ok && (d > 0.0);
-                const double dinv = 1.0 / d;
-                const bool piv = (t == pv);
-                const double fd = Krow[0] * dinv;
-                // K_tj <- al K_tj + be K_pj : (al, be) = (1, -K_tp/d) off the pivot row and (0, 1/d)
-                // on it (0 * K_tj is exact for finite K); column pv <- K_tp/d, or -1/d on the pivot
-                const double al = piv ? 0.0 : 1.0, be = piv ? dinv : -fd;
-                const double k0 = piv ? -dinv : fd;
+#pragma nounroll
+                for (int pv = 0; pv < NN; ++pv) {
+                    __syncthreads();
+                    const int o = pv & 1;
+                    const double* prow = s_sw + o * SB + o + pv;
+                    // the rotated pivot row as 20 aligned 16-byte reads, issued ahead of their FMAs
+                    const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
+                    double2 pr[NN / 2];
 #pragma unroll
-                for (int j = 1; j < NN; ++j) Krow[j - 1] = fma(be, prow[j], al * Krow[j]);
-                Krow[NN - 1] = k0;   // rotate: the pivot column moves to the end
+                    for (int i = 0; i < NN / 2; ++i) pr[i] = prow2[i];
+                    const double d = pr[0].x;
+                    ok = ok && (d > 0.0);
+                    const double dinv = rcp_nr(d);
+                    const bool piv = (t == pv);
+                    const double fd = Krow[0] * dinv;
+                    // (a single-FMA form with c = 1/d - 1 on the pivot row was measured: no faster --
+                    // the loop is latency-bound -- and it costs polish accuracy at large pivots)
+                    const double al = piv ? 0.0 : 1.0, be = piv ? dinv : -fd;
+                    const double k0 = piv ? -dinv : fd;
+                    const double n0 = fma(be, pr[0].y, al * Krow[1]);
+                    if (t < NN) {
+                        double* nb = s_sw + (o ^ 1) * SB + (o ^ 1);
+                        nb[t] = n0;
+                        nb[t + NN] = n0;
+                    }
+#pragma unroll
+                    for (int j = 2; j < NN; ++j) Krow[j - 1] = fma(be, (j & 1) ? pr[j >> 1].y : pr[j >> 1].x, al * Krow[j]);
+                    // keep ~8 reads in flight ahead of the FMAs (the default schedule waits on each)
+                    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+                    for (int i = 0; i < NN / 2 - 8; ++i) {
+                        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    }
+                    Krow[0] = n0;
+                    Krow[NN - 1] = k0;   // rotate: the pivot column moves to the end
+                }
             }
 #pragma unroll
             for (int j = 0; j < NN; ++j) Krow[j] = -Krow[j];
+            toc(cyc_sweep);
             if (!ok) {
                 if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
                 // failed reduced-KKT factorization = unsuccessful polish (polish.c): the ADMM
@@ -556,7 +605,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
                     zr = nzr;
                     if (--chk == 0) {
                         chk = c.check_interval;
+                        tic();
                         r = residuals(x, zb, zr, yb, yr);
+                        toc(cyc_res);
+                        ++n_res;
                         if (r.pr <= escale * r.eps_p && r.dr <= escale * r.eps_d) { converged = true; break; }
                         if (c.adaptive_rho) {
                             double pn = fmax(r.axs, r.zs);
@@ -597,6 +649,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
             }
 
             // ---- PH_POLISH: Krow = row of M^{-1}, M = P + dI + Ar'Ar/d (eliminated reduced KKT) ----
+            tic();
+            pol_open = true;
             {
                 const double bb = actb < 0 ? slb : (actb > 0 ? sub : 0.0);
                 const double br = actr < 0 ? slr : (actr > 0 ? sur : 0.0);
@@ -695,8 +749,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
             a.wsWarm[2 * (size_t)b] = rho;
             a.wsWarm[2 * (size_t)b + 1] = okst ? 1.0 : 0.0;
         }
+        if (pol_open) toc(cyc_pol);
         stamp(8, nfact);
         stamp(10, ps);
+        stamp(11, cyc_res);
+        stamp(12, cyc_sweep);
+        stamp(13, cyc_pol);
+        stamp(14, n_res);
     } else {
         status = early;
         iter = 0;
@@ -742,6 +801,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     }
     double obj = block_sum(op);
     stamp(7, __builtin_amdgcn_s_memtime());
+    stamp(3, __builtin_amdgcn_s_memrealtime());
     const double nan = __builtin_nan("");
     double uc0 = good ? Ubuf[0] : s_up[0], uc1 = good ? Ubuf[1] : s_up[1];
     if (CLOSED) {
