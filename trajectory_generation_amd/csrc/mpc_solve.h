@@ -25,7 +25,7 @@ namespace tgmpc {
 // update, history).  A_k, B_k, g_k are read from a.Ad / a.Bd / a.gd ([B,N,36], [B,N,12], [B,N,6]).
 // =====================================================================================
 template <int NN, bool CLOSED>
-__global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArgs a) {
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(2))) void solve_kernel(const KArgs a) {
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
@@ -45,6 +45,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     __shared__ double s_sc[(NM + 1) * 2];
     __shared__ __attribute__((aligned(16))) double s_ex[6 * NN];   // exchange / broadcast buffers
     __shared__ __attribute__((aligned(16))) double s_sw[2 * (2 * NN + 2)];   // sweep pivot columns
+    __shared__ double s_F[2 * 3 * 16 * ((NN + 15) / 16)];                    // condensing: F_k rows
     __shared__ double s_red[16 * WAVES];
     __shared__ int s_flag[4];
 
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     // exchange buffers start at zero: entries >= n are the zero padding the unguarded
     // register loops over the full capacity NN rely on
     for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
+    for (int i = t; i < 2 * 3 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     if (CLOSED) {
         if (t < 6) s_x0[t] = a.x_state[6 * b + t];
         if (t < 2) s_up[t] = a.u_state[2 * b + t];
@@ -189,16 +191,39 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
     // P = sum_k G_k' C_k' 2W C_k G_k and q = sum_k G_k' C_k' 2W e_k, accumulated stage by stage:
     // lane t carries column t of the input sensitivity G_k (6-vector); the free response xh_k and
     // its tracking errors e_k are uniform and computed by every lane.  With the weights split as
-    // sqrt(2W) into F = sqrt(2W) C G, each stage adds F_t F_j (3 FMAs per entry) -- a product that is
-    // commutative, so P stays bitwise symmetric.
+    // sqrt(2W), F_k = sqrt(2W) C_k G_k (3 x n per stage) and P = sum_k F_k' F_k.
+    //   one wave (NN <= 64): P accumulates on the matrix cores -- per stage one k=4 step of
+    //     v_mfma_f64_16x16x4 per upper-triangle 16x16 tile (rows 0..2 of the step = F_k, row 3 = 0);
+    //     each lane reads just the 1-3 F values of its operand slots;
+    //   two waves (NN = 80): each lane accumulates its row, F_t F_j (3 FMAs per entry).
+    // Both give an exactly symmetric P (each unordered pair is formed once / by a commutative product).
     double Prow[NN];
-#pragma unroll
-    for (int j = 0; j < NN; ++j) Prow[j] = 0.0;
     double qi = 0.0;
+    auto opaque_t = [&]() -> int {
+        int r;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t < NN ? t : 0));
+        return r;
+    };
+    auto paddr = [&](int j, int tt) -> int {   // packed upper triangle: P(i, j), i <= j
+        return (j < tt) ? (j * NN - (j * (j - 1)) / 2 - j + tt) : (tt * NN - (tt * (tt - 1)) / 2 - tt + j);
+    };
     {
         const double sw0 = sqrt(2.0 * c.q_c), sw1 = sqrt(2.0 * c.q_phi), sw2 = sqrt(2.0 * c.q_vx);
         double xh[6], G[6] = {0, 0, 0, 0, 0, 0};
         for (int i = 0; i < 6; ++i) xh[i] = s_x0[i];
+        constexpr int NB = (NN + 15) / 16;          // 16-wide column blocks (MFMA path)
+        constexpr int NTILE = NB * (NB + 1) / 2;
+        constexpr int FS = 16 * NB;
+        typedef double d4 __attribute__((ext_vector_type(4)));
+        d4 acc[WAVES == 1 ? NTILE : 1];
+        if constexpr (WAVES == 1) {
+#pragma unroll
+            for (int i = 0; i < NTILE; ++i) acc[i] = d4{0.0, 0.0, 0.0, 0.0};
+        } else {
+#pragma unroll
+            for (int j = 0; j < NN; ++j) Prow[j] = 0.0;
+        }
+        const int mr = (t >> 4) & 3, mc = t & 15;   // MFMA operand slot of this lane: k-row, column
         for (int k = 0; k < N; ++k) {
             const double* Ak = cA + 36 * k;
             // free response xh_{k+1} = A_k xh_k + g_k (uniform)
@@ -239,15 +264,47 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
             const double e2 = xh[3] - s_vref[k1];
             const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
             qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
-            double* buf = s_ex + (xb & 1) * 3 * NN;   // 2 rotating slots of 3*NN
-            xb++;
-            if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
-            __syncthreads();
+            if constexpr (WAVES == 1) {
+                double* fb = s_F + (k & 1) * 3 * FS;    // 2 rotating slots, zero beyond n
+                if (own) { fb[t] = F0; fb[FS + t] = F1; fb[2 * FS + t] = F2; }
+                __syncthreads();
+                double opv[NB];
 #pragma unroll
-            for (int j = 0; j < NN; ++j)
-                Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
+                for (int ib = 0; ib < NB; ++ib) opv[ib] = (mr < 3) ? fb[mr * FS + 16 * ib + mc] : 0.0;
+                int ti = 0;
+#pragma unroll
+                for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+                    for (int jb = ib; jb < NB; ++jb, ++ti)
+                        acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(opv[ib], opv[jb], acc[ti], 0, 0, 0);
+            } else {
+                double* buf = s_ex + (xb & 1) * 3 * NN;   // 2 rotating slots of 3*NN
+                xb++;
+                if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < NN; ++j)
+                    Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
+            }
         }
         __syncthreads();
+        if constexpr (WAVES == 1) {
+            // accumulator tiles (lane: row 16 ib + mr + 4 reg, column 16 jb + mc) -> packed P -> rows
+            int ti = 0;
+#pragma unroll
+            for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+                for (int jb = ib; jb < NB; ++jb, ++ti)
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) {
+                        const int i = 16 * ib + ((t >> 4) & 3) + 4 * reg, j = 16 * jb + mc;
+                        if (i <= j && j < NN) s_P[i * NN - (i * (i - 1)) / 2 + (j - i)] = acc[ti][reg];
+                    }
+            __syncthreads();
+            const int tt = opaque_t();
+#pragma unroll
+            for (int j = 0; j < NN; ++j) Prow[j] = own ? s_P[paddr(j, tt)] : 0.0;
+        }
     }
     // input penalties U'RU and dU'Rd dU (dU_0 = U_0 - u_prev)
     double Rs[4], Rds[4];
@@ -367,19 +424,6 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) void solve_kernel(const KArg
                 if (j >= t) s_P[rt + j] = own ? Prow[j] : 0.0;
         }
         __syncthreads();
-        // Address of P(t, j) for a compile-time j: column segment (j < t) or row segment (j >= t).
-        // `opaque_t` re-materializes t through an asm move at each use site, so the compiler cannot
-        // hoist the NN per-lane addresses / compare masks out of the solver loops (that costs
-        // ~NN VGPRs + 2 NN SGPRs of loop-invariant state and spills everything else).
-        auto opaque_t = [&]() -> int {
-            int r;
-            asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t < NN ? t : 0));
-            return r;
-        };
-        auto paddr = [&](int j, int tt) -> int {
-            return (j < tt) ? (j * NN - (j * (j - 1)) / 2 - j + tt) : (tt * NN - (tt * (tt - 1)) / 2 - tt + j);
-        };
-
         stamp(5, __builtin_amdgcn_s_memtime());
         // ---- helpers over the scaled problem ----------------------------------------
         // A x (box, rate) for the vector v owned row-wise
