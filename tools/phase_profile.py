@@ -13,11 +13,11 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     vref = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=dev).contiguous()
     cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
     for t in range(warm):
-        TB.closed_loop_step(x, u, paths, vref, cfg)
+        TB.closed_loop_step(x, u, paths, vref, cfg, None, t)
     dbg = torch.zeros((B, 16), dtype=torch.int64, device=dev)
     _lib.lib().traj_debug_set_stamps(C.c_void_p(dbg.data_ptr()))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(); TB.closed_loop_step(x, u, paths, vref, cfg); e1.record()
+    e0.record(); TB.closed_loop_step(x, u, paths, vref, cfg, None, warm); e1.record()
     torch.cuda.synchronize()
     _lib.lib().traj_debug_set_stamps(None)
     d = dbg.cpu().numpy()
@@ -53,4 +53,4 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     print("in-kernel clock (median over instances): %.2f GHz" % np.median(clk))
 
 if __name__ == "__main__":
-    main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0)
+    main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0, warm=int(sys.argv[2]) if len(sys.argv) > 2 else 5)

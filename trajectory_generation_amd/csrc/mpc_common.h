@@ -69,7 +69,8 @@ struct KArgs {
     double* wsA;             // linearization outputs (workspace): [B,N,6,6], [B,N,6,2], [B,N,6]
     double* wsB;
     double* wsg;
-    double* wsWarm;          // closed loop: per instance [rho, valid] of the previous step
+    double* wsWarm;          // closed loop: per instance [rho, valid, ADMM iterations, 0] of the previous step
+    const int* perm;         // closed loop: instance order (longest previous solve first), or null
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

@@ -45,13 +45,15 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     __shared__ double s_sc[(NM + 1) * 2];
     __shared__ __attribute__((aligned(16))) double s_ex[6 * NN];   // exchange / broadcast buffers
     __shared__ __attribute__((aligned(16))) double s_sw[2 * (2 * NN + 2)];   // sweep pivot columns
-    __shared__ double s_F[2 * 3 * 16 * ((NN + 15) / 16)];                    // condensing: F_k rows
+    __shared__ double s_F[2 * 4 * 16 * ((NN + 15) / 16)];                    // condensing: F_k rows
     __shared__ double s_red[16 * WAVES];
     __shared__ int s_flag[4];
 
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
-    const int b = blockIdx.x;
+    // closed loop: workgroups take instances longest-previous-solve first (LPT order), so the
+    // slowest solves start at once instead of in the last dispatch round
+    const int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
     const int t = threadIdx.x;
     const int lane = t & 63, wid = t >> 6;
     const int N = c.N, n = 2 * N;
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // exchange buffers start at zero: entries >= n are the zero padding the unguarded
     // register loops over the full capacity NN rely on
     for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
-    for (int i = t; i < 2 * 3 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
+    for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     if (CLOSED) {
         if (t < 6) s_x0[t] = a.x_state[6 * b + t];
         if (t < 2) s_up[t] = a.u_state[2 * b + t];
@@ -239,22 +241,20 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             for (int r = 0; r < 6; ++r) xh[r] = xn[r];
             // input sensitivities: columns of inputs applied before stage k propagate, stage k's
             // inputs enter through B_k
-            if (own) {
-                if (t < 2 * k) {
-                    double Gn[6];
+            // (branch-free: every lane forms A_k G, then selects -- no divergent exec juggling)
+            {
+                const bool prop = own && (t < 2 * k), enter = own && (kk == k);
+                double Gn[6];
 #pragma unroll
-                    for (int r = 0; r < 6; ++r) {
-                        double v = 0.0;
+                for (int r = 0; r < 6; ++r) {
+                    double v = 0.0;
 #pragma unroll
-                        for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], G[cc], v);
-                        Gn[r] = v;
-                    }
-#pragma unroll
-                    for (int r = 0; r < 6; ++r) G[r] = Gn[r];
-                } else if (kk == k) {
-#pragma unroll
-                    for (int r = 0; r < 6; ++r) G[r] = cB[12 * k + 2 * r + ch];
+                    for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], G[cc], v);
+                    const double bv = cB[12 * k + 2 * r + ch];
+                    Gn[r] = prop ? v : (enter ? bv : G[r]);
                 }
+#pragma unroll
+                for (int r = 0; r < 6; ++r) G[r] = Gn[r];
             }
             // stage k+1 outputs: tracking errors of the free response, weighted sensitivities
             const int k1 = k + 1;
@@ -265,12 +265,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
             qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
             if constexpr (WAVES == 1) {
-                double* fb = s_F + (k & 1) * 3 * FS;    // 2 rotating slots, zero beyond n
+                double* fb = s_F + (k & 1) * 4 * FS;    // 2 rotating slots; row 3 and columns >= n stay 0
                 if (own) { fb[t] = F0; fb[FS + t] = F1; fb[2 * FS + t] = F2; }
                 __syncthreads();
                 double opv[NB];
 #pragma unroll
-                for (int ib = 0; ib < NB; ++ib) opv[ib] = (mr < 3) ? fb[mr * FS + 16 * ib + mc] : 0.0;
+                for (int ib = 0; ib < NB; ++ib) opv[ib] = fb[mr * FS + 16 * ib + mc];
                 int ti = 0;
 #pragma unroll
                 for (int ib = 0; ib < NB; ++ib)
@@ -364,39 +364,45 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     stamp(4, __builtin_amdgcn_s_memtime());
     if (early < 0) {
         // ---- 4a. Ruiz equilibration + cost scaling (OSQP scale_data) ---------------
+        // Prow / qi carry D P D and D q; the cost factor cs (uniform, > 0) is applied once at the end,
+        // so the column norms of the scaled P are cs * cn with cn = max_j |Prow_j|, tracked in the
+        // scaling pass itself (one pass over the row per iteration instead of four).
         double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0;
+        double cn = 0.0;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) cn = fmax(cn, fabs(Prow[j]));
         for (int it = 0; it < c.scaling_iters; ++it) {
             double Er_up = exch(Er, +2);     // E of rate row t+2
             double D_dn = exch(D, -2);       // D of variable t-2
             double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
-            double pn = 0.0;
-#pragma unroll
-            for (int j = 0; j < NN; ++j) pn = fmax(pn, fabs(Prow[j]));
+            const double pn = cs * cn;
             double coln = fmax(pn, fmax(fabs(a_b), fmax(fabs(a_r), fabs(a_rp))));
             double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
             double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
             double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
             double* Dv = bcast(Dt);
+            cn = 0.0;
 #pragma unroll
-            for (int j = 0; j < NN; ++j) Prow[j] *= Dt * Dv[j];
+            for (int j = 0; j < NN; ++j) {
+                const double v = Prow[j] * (Dt * Dv[j]);
+                Prow[j] = v;
+                cn = fmax(cn, fabs(v));
+            }
             qi *= Dt;
             D *= Dt;
             Eb *= Etb;
             Er *= Etr;
-            // cost scaling
-            double cn = 0.0;
-#pragma unroll
-            for (int j = 0; j < NN; ++j) cn = fmax(cn, fabs(Prow[j]));
-            double mean = block_sum(own ? cn : 0.0) / n;
-            double qv[1] = {own ? fabs(qi) : 0.0};
+            // cost scaling of the scaled data cs (P, q)
+            double mean = block_sum(own ? cs * cn : 0.0) / n;
+            double qv[1] = {own ? fabs(cs * qi) : 0.0};
             block_max(qv);
             double ct = fmax(mean, limit_scaling(qv[0]));
             ct = 1.0 / limit_scaling(ct);
-#pragma unroll
-            for (int j = 0; j < NN; ++j) Prow[j] *= ct;
-            qi *= ct;
             cs *= ct;
         }
+#pragma unroll
+        for (int j = 0; j < NN; ++j) Prow[j] *= cs;
+        qi *= cs;
         const double csinv = 1.0 / cs;   // uniform
         const double D_dn = exch(D, -2), Er_up = exch(Er, +2);
         const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
@@ -514,7 +520,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         // lengthen the iteration tail).  mpc_6stati.py:256 asks OSQP for warm_start=True, a no-op
         // there because a new Problem is built every call; the polished optimum does not depend on rho.
         if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {
-            const double* wv = a.wsWarm + 2 * (size_t)b;
+            const double* wv = a.wsWarm + 4 * (size_t)b;
             if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
         }
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
@@ -790,8 +796,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         xsol = cold(C_D) * x;
         if (CLOSED && a.wsWarm && t == 0) {
             const bool okst = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
-            a.wsWarm[2 * (size_t)b] = rho;
-            a.wsWarm[2 * (size_t)b + 1] = okst ? 1.0 : 0.0;
+            a.wsWarm[4 * (size_t)b] = rho;
+            a.wsWarm[4 * (size_t)b + 1] = okst ? 1.0 : 0.0;
+            a.wsWarm[4 * (size_t)b + 2] = (double)(iter > c.max_iter ? c.max_iter : iter);
         }
         if (pol_open) toc(cyc_pol);
         stamp(8, nfact);
@@ -803,7 +810,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     } else {
         status = early;
         iter = 0;
-        if (CLOSED && a.wsWarm && t == 0) a.wsWarm[2 * (size_t)b + 1] = 0.0;
+        if (CLOSED && a.wsWarm && t == 0) {
+            a.wsWarm[4 * (size_t)b + 1] = 0.0;
+            a.wsWarm[4 * (size_t)b + 2] = 0.0;
+        }
     }
 
     stamp(6, __builtin_amdgcn_s_memtime());

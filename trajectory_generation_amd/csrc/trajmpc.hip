@@ -125,6 +125,33 @@ __global__ void ref_window_kernel(PathArgs pa, int B, int N, double Ts, const do
     }
 }
 
+// ---------------------------------------------------------------- closed-loop solve order
+// Counting sort of the instances by their previous ADMM iteration count (25-iteration buckets,
+// descending): a permutation whatever the workspace holds (non-finite keys land in bucket 0).
+__global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, int* perm) {
+    constexpr int NBK = 512;
+    __shared__ int hist[NBK];
+    __shared__ int offs[NBK];
+    const int t = threadIdx.x;
+    for (int i = t; i < NBK; i += 1024) hist[i] = 0;
+    __syncthreads();
+    auto key = [&](int i) -> int {
+        const double v = fmin(fmax(warm[4 * (size_t)i + 2] / 25.0, 0.0), (double)(NBK - 1));
+        return (int)v;
+    };
+    for (int i = t; i < B; i += 1024) atomicAdd(&hist[key(i)], 1);
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int k = NBK - 1; k >= 0; --k) {
+            offs[k] = acc;
+            acc += hist[k];
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < B; i += 1024) perm[atomicAdd(&offs[key(i)], 1)] = i;
+}
+
 // ---------------------------------------------------------------- MPC dispatch
 
 // per-capacity launchers (mpc_inst.hip compiled once per NN)
@@ -302,7 +329,8 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
     if (B < 0 || N < 0) return 0;
-    return ((size_t)B * (size_t)N * 54 + (size_t)B * 2) * sizeof(double);
+    // A/B/g hand-off (54 N doubles), warm-start record (4 doubles), closed-loop order (1 int)
+    return ((size_t)B * (size_t)N * 54 + (size_t)B * 4) * sizeof(double) + (((size_t)B * sizeof(int) + 7) & ~(size_t)7);
 }
 
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
@@ -368,6 +396,12 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.wsg = a.wsB + (size_t)B * c->N * 12;
     a.wsWarm = a.wsg + (size_t)B * c->N * 6;
     a.Ad = a.wsA; a.Bd = a.wsB; a.gd = a.wsg;
+    if (t > 0) {
+        // order this step's solves by the previous step's iteration counts (longest first)
+        int* perm = (int*)(a.wsWarm + (size_t)B * 4);
+        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, (const double*)a.wsWarm, B, perm);
+        a.perm = perm;
+    }
     return launch_mpc(a, (hipStream_t)stream, 2);
 }
 
