@@ -111,10 +111,11 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
                              const double* phiref, double* out /*[B]*/, void* stream);
 
 /* Device workspace the MPC step needs for B instances of horizon N: the linearization A_k, B_k, g_k
- * handed from the linearize kernel to the solve kernel (B * N * 54 doubles), then the closed-loop
- * record of the previous step (B * 4 doubles: rho, valid flag, ADMM iterations) and the closed-loop
- * solve order (B ints, longest previous solve first).  Pass the same buffer to every
- * traj_closed_loop_step of one run; step t = 0 starts cold. */
+ * handed from the linearize kernels to the solve kernel (B * N * 54 doubles), the rollout record
+ * (x_k, f_k) per stage (B * N * 12 doubles), then the closed-loop record of the previous step
+ * (B * 4 doubles: rho, valid flag, ADMM iterations) and the closed-loop solve order (B ints,
+ * longest previous solve first).  Pass the same buffer to every traj_closed_loop_step of one run;
+ * step t = 0 starts cold. */
 size_t traj_mpc_workspace_bytes(int B, int N);
 
 /* ---- the MPC step (mpc_6stati.py:120-275) for B independent instances ----

@@ -69,6 +69,7 @@ struct KArgs {
     double* wsA;             // linearization outputs (workspace): [B,N,6,6], [B,N,6,2], [B,N,6]
     double* wsB;
     double* wsg;
+    double* wsXF;            // rollout record (x_k, f_k) per stage: [B,N,12]
     double* wsWarm;          // closed loop: per instance [rho, valid, ADMM iterations, 0] of the previous step
     const int* perm;         // closed loop: instance order (longest previous solve first), or null
 };

@@ -1,6 +1,5 @@
 // mpc_inst.hip -- one translation unit per horizon capacity (compiled with -DTGMPC_NN=<NN>), so
 // the fully unrolled instantiations of the MPC kernels build in parallel.
-#include "mpc_linearize.h"
 #include "mpc_solve.h"
 
 #ifndef TGMPC_NN
@@ -12,20 +11,13 @@
 
 namespace tgmpc {
 
-// mode 0: MPC step (linearize -> solve), 1: QP only (A/B/g given), 2: closed-loop step
+// mode 0: MPC step, 1: QP only (A/B/g given), 2: closed-loop step (the linearization launches are
+// issued by the caller, trajmpc.hip)
 int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
     constexpr int NN = TGMPC_NN;
-    constexpr int NM = NN / 2;
-    dim3 grid(a.B), sblock(((NN + 63) / 64) * 64), lblock(64);
-    if (mode == 0) {
-        hipLaunchKernelGGL((linearize_kernel<NM, false>), grid, lblock, 0, st, a);
-        hipLaunchKernelGGL((solve_kernel<NN, false>), grid, sblock, 0, st, a);
-    } else if (mode == 1) {
-        hipLaunchKernelGGL((solve_kernel<NN, false>), grid, sblock, 0, st, a);
-    } else {
-        hipLaunchKernelGGL((linearize_kernel<NM, true>), grid, lblock, 0, st, a);
-        hipLaunchKernelGGL((solve_kernel<NN, true>), grid, sblock, 0, st, a);
-    }
+    dim3 grid(a.B), sblock(((NN + 63) / 64) * 64);
+    if (mode == 2) hipLaunchKernelGGL((solve_kernel<NN, true>), grid, sblock, 0, st, a);
+    else hipLaunchKernelGGL((solve_kernel<NN, false>), grid, sblock, 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

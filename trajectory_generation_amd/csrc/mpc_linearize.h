@@ -1,106 +1,192 @@
-// mpc_linearize.h -- kernel 1 of the MPC step: nominal rollout + central-difference linearization.
+// mpc_linearize.h -- stage 1 of the MPC step: nominal rollout + central-difference linearization.
 //
 // Reference: MPC/mpc_6stati.py:165-178 (rollout and the N linearization points), :73-97
 // (numerical_jacobian, eps = 1e-5), :99-109 (A = I + Ts Jx, B = Ts Ju, g = x + Ts f - A x - B u).
-// One 64-lane wave per instance.  Lane 0 runs the (serial) Euler rollout; the 6 non-trivial
-// Jacobian columns of every stage (phi, vx, vy, omega, d, delta) are then independent items, one
-// lane each, 2 f_cont evaluations per item.  Columns X and Y are exactly zero (f does not read
-// X, Y, so the reference's f(x+dx) - f(x-dx) is 0.0 bit for bit) and are not evaluated.
-// A, B, g are staged in LDS and written to the workspace as [B,N,36], [B,N,12], [B,N,6] float64,
-// where the solve kernel (mpc_solve.h) reads them back (L2 / Infinity-Cache resident).
+//
+// Two launches, each with every lane busy:
+//   rollout_kernel  one THREAD per instance runs the serial Euler rollout x_{k+1} = x_k + Ts f(x_k, u)
+//                   (u = u_prev, constant) and records (x_k, f_k) per stage: [B, N, 12].
+//   jac_kernel      one thread per (instance, stage) forms the 6 non-trivial Jacobian columns (phi, vx,
+//                   vy, omega, d, delta) by central differences and writes A_k, B_k, g_k to the
+//                   workspace as [B,N,36], [B,N,12], [B,N,6] (read back by the solve kernel).
+// Columns X, Y are exactly zero (f does not read X, Y: the reference's f(x+dx) - f(x-dx) is 0.0) and
+// are not evaluated.  The difference quotients reuse the parts of f that a perturbation leaves
+// unchanged (the tire forces for a phi or d step, the rear force and sin/cos(phi) for a delta step,
+// sin/cos(phi) and sin/cos(delta) for vx / vy / omega steps): each reused value is the one f would
+// recompute from identical inputs, so the quotients equal the full evaluations.  The shared parts
+// are formed from the unperturbed state as the state columns see it (x_i + 0.0, the reference's
+// x + dx); the input columns, where the reference passes x itself, see the same values unless a
+// component is exactly -0.0 -- then those two columns are evaluated on the exact vectors.
 #pragma once
 #include "mpc_common.h"
 
 namespace tgmpc {
 
-template <int NM, bool CLOSED>
-__global__ __launch_bounds__(64) void linearize_kernel(const KArgs a) {
-    __shared__ double s_xbar[(NM + 1) * 6];
-    __shared__ double s_fbar[NM * 6];
-    __shared__ double s_A[NM * 36];
-    __shared__ double s_B[NM * 12];
-    __shared__ double s_g[NM * 6];
-    __shared__ double s_x0[6], s_up[2];
-
+template <bool CLOSED>
+__global__ __launch_bounds__(64) void rollout_kernel(const KArgs a) {
+    const int b = blockIdx.x * 64 + threadIdx.x;
+    if (b >= a.B) return;
     const traj_vehicle_params& p = a.p;
-    const int b = blockIdx.x;
-    const int t = threadIdx.x;
     const int N = a.c.N;
     const double Ts = a.c.Ts;
-
-    if (CLOSED) {
-        if (t < 6) s_x0[t] = a.x_state[6 * b + t];
-        if (t < 2) s_up[t] = a.u_state[2 * b + t];
-    } else {
-        if (t < 6) s_x0[t] = a.x0[6 * b + t];
-        if (t < 2) s_up[t] = a.u_prev[2 * b + t];
-    }
-    __syncthreads();
-
-    // nominal rollout (:165-172), constant input u_prev
-    if (t == 0) {
-        double x[6], f[6], sd, cd;
-        sincos(s_up[1], &sd, &cd);
+    const double* xs = CLOSED ? a.x_state + 6 * (size_t)b : a.x0 + 6 * (size_t)b;
+    const double* us = CLOSED ? a.u_state + 2 * (size_t)b : a.u_prev + 2 * (size_t)b;
+    double x[6], f[6];
+    for (int i = 0; i < 6; ++i) x[i] = xs[i];
+    const double u0 = us[0], u1 = us[1];
+    double sd, cd;
+    sincos(u1, &sd, &cd);
+    double* rec = a.wsXF + (size_t)b * N * 12;
+    for (int k = 0; k < N; ++k) {
+        f_cont_sc(p, x, u0, u1, sd, cd, f);
         for (int i = 0; i < 6; ++i) {
-            x[i] = s_x0[i];
-            s_xbar[i] = x[i];
-        }
-        for (int k = 0; k < N; ++k) {
-            f_cont_sc(p, x, s_up[0], s_up[1], sd, cd, f);
-            for (int i = 0; i < 6; ++i) {
-                s_fbar[6 * k + i] = f[i];
-                x[i] = x[i] + Ts * f[i];
-                s_xbar[6 * (k + 1) + i] = x[i];
-            }
+            rec[12 * k + i] = x[i];
+            rec[12 * k + 6 + i] = f[i];
+            x[i] = x[i] + Ts * f[i];
         }
     }
-    __syncthreads();
+}
 
-    // Jacobian columns (:73-97): item = (stage k, column col), col 0..5 states, 6..7 inputs
+// parts of the tire model (mpc_6stati.py:25-53), split so perturbations can reuse them
+struct Tire {
+    double vx_eff, atf, atr;   // vx_eff, atan2(omega lf + vy, vx_eff), atan2(omega lr - vy, vx_eff)
+};
+__device__ __forceinline__ Tire tire_angles(const VP& p, double vx, double vy, double omega) {
+    Tire r;
+    const double avx = fabs(vx);
+    const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
+    r.vx_eff = np_sign(vx) * mx;
+    r.atf = atan2(omega * p.lf + vy, r.vx_eff);
+    r.atr = atan2(omega * p.lr - vy, r.vx_eff);
+    return r;
+}
+__device__ __forceinline__ double front_force(const VP& p, double atf, double delta) {
+    const double alpha_f = clampd(-atf + delta, -p.maxAlpha, p.maxAlpha);
+    return p.Df * sin(p.Cf * atan(p.Bf * alpha_f));
+}
+__device__ __forceinline__ double rear_force(const VP& p, double atr) {
+    const double alpha_r = clampd(atr, -p.maxAlpha, p.maxAlpha);
+    return p.Dr * sin(p.Cr * atan(p.Br * alpha_r));
+}
+__device__ __forceinline__ double long_force(const VP& p, double vx, double d) {
+    return (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
+}
+// mpc_6stati.py:55-71 from its parts
+__device__ __forceinline__ void f_parts(const VP& p, double vx, double vy, double omega, double sphi, double cphi,
+                                        double sd, double cd, double Fy_f, double Fy_r, double Frx, double* xd) {
+    xd[0] = vx * cphi - vy * sphi;
+    xd[1] = vx * sphi + vy * cphi;
+    xd[2] = omega;
+    xd[3] = (1.0 / p.m) * (Frx - Fy_f * sd + p.m * vy * omega);
+    xd[4] = (1.0 / p.m) * (Fy_r + Fy_f * cd - p.m * vx * omega);
+    xd[5] = (1.0 / p.Iz) * (Fy_f * p.lf * cd - Fy_r * p.lr);
+}
+// full f at a state/input point with shared sin/cos
+__device__ __forceinline__ void f_full(const VP& p, double vx, double vy, double omega, double sphi, double cphi,
+                                       double d, double delta, double sd, double cd, double* xd) {
+    const Tire tr = tire_angles(p, vx, vy, omega);
+    f_parts(p, vx, vy, omega, sphi, cphi, sd, cd, front_force(p, tr.atf, delta), rear_force(p, tr.atr),
+            long_force(p, vx, d), xd);
+}
+
+template <bool CLOSED>
+__global__ __launch_bounds__(64) void jac_kernel(const KArgs a) {
+    const int N = a.c.N;
+    const int idx = blockIdx.x * 64 + threadIdx.x;
+    if (idx >= a.B * N) return;
+    const int b = idx / N, k = idx - b * N;
+    const traj_vehicle_params& p = a.p;
+    const double Ts = a.c.Ts;
     const double eps = 1e-5;
-    for (int it = t; it < 8 * N; it += 64) {
-        const int k = it >> 3, col = it & 7;
-        double J[6] = {0, 0, 0, 0, 0, 0};
-        if (col >= 2) {
-            double xp[6], xm[6], up[2], um[2], fp[6], fm[6];
-            // exactly the reference's vectors: the perturbed argument is x + dx / x - dx with
-            // dx = eps e_col (so x_i + 0.0 elsewhere), the other argument is passed unchanged
-            const bool on_x = col < 6;
-            for (int i = 0; i < 6; ++i) {
-                const double xi = s_xbar[6 * k + i], d = (i == col) ? eps : 0.0;
-                xp[i] = on_x ? xi + d : xi;
-                xm[i] = on_x ? xi - d : xi;
-            }
-            for (int i = 0; i < 2; ++i) {
-                const double ui = s_up[i], d = (i + 6 == col) ? eps : 0.0;
-                up[i] = on_x ? ui : ui + d;
-                um[i] = on_x ? ui : ui - d;
-            }
-            f_cont(p, xp, up, fp);
-            f_cont(p, xm, um, fm);
-            for (int r = 0; r < 6; ++r) J[r] = (fp[r] - fm[r]) / (2.0 * eps);
-        }
-        // :106-107  Ad = I + Ts Jx ; Bd = Ts Ju
-        for (int r = 0; r < 6; ++r) {
-            if (col < 6) s_A[k * 36 + r * 6 + col] = ((r == col) ? 1.0 : 0.0) + Ts * J[r];
-            else s_B[k * 12 + r * 2 + (col - 6)] = Ts * J[r];
+    const double* rec = a.wsXF + ((size_t)b * N + k) * 12;
+    const double* us = CLOSED ? a.u_state + 2 * (size_t)b : a.u_prev + 2 * (size_t)b;
+    double xb[6], fb[6];
+    for (int i = 0; i < 6; ++i) {
+        xb[i] = rec[i];
+        fb[i] = rec[6 + i];
+    }
+    const double d = us[0], de = us[1];
+    // unperturbed components as the reference's x + dx carries them (x_i + 0.0)
+    const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
+    double sphi, cphi, sd, cd;
+    sincos(phi, &sphi, &cphi);
+    sincos(de, &sd, &cd);
+    const Tire t0 = tire_angles(p, vx, vy, om);
+    const double Ff0 = front_force(p, t0.atf, de), Fr0 = rear_force(p, t0.atr), Fx0 = long_force(p, vx, d);
+
+    double J[6][6];   // J[col - 2][row]
+    double fp[6], fm[6];
+    // phi: only sin/cos(phi) change
+    {
+        double sp, cp, sm, cm;
+        sincos(xb[2] + eps, &sp, &cp);
+        sincos(xb[2] - eps, &sm, &cm);
+        f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
+        f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
+        for (int r = 0; r < 6; ++r) J[0][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    // vx, vy, omega: tire forces recomputed, sin/cos shared
+    {
+        f_full(p, xb[3] + eps, vy, om, sphi, cphi, d, de, sd, cd, fp);
+        f_full(p, xb[3] - eps, vy, om, sphi, cphi, d, de, sd, cd, fm);
+        for (int r = 0; r < 6; ++r) J[1][r] = (fp[r] - fm[r]) / (2.0 * eps);
+        f_full(p, vx, xb[4] + eps, om, sphi, cphi, d, de, sd, cd, fp);
+        f_full(p, vx, xb[4] - eps, om, sphi, cphi, d, de, sd, cd, fm);
+        for (int r = 0; r < 6; ++r) J[2][r] = (fp[r] - fm[r]) / (2.0 * eps);
+        f_full(p, vx, vy, xb[5] + eps, sphi, cphi, d, de, sd, cd, fp);
+        f_full(p, vx, vy, xb[5] - eps, sphi, cphi, d, de, sd, cd, fm);
+        for (int r = 0; r < 6; ++r) J[3][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    // d: only the longitudinal force changes
+    {
+        f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d + eps), fp);
+        f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d - eps), fm);
+        for (int r = 0; r < 6; ++r) J[4][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    // delta: front force and sin/cos(delta) change
+    {
+        double sp, cp, sm, cm;
+        sincos(de + eps, &sp, &cp);
+        sincos(de - eps, &sm, &cm);
+        f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
+        f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
+        for (int r = 0; r < 6; ++r) J[5][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    // a -0.0 among the components the input columns pass through: evaluate those two columns on the
+    // reference's exact vectors, f(x, u +- du) with u_other + 0.0 (signed zeros then match too)
+    if (__builtin_signbit(xb[2]) && xb[2] == 0.0 || __builtin_signbit(xb[3]) && xb[3] == 0.0 ||
+        __builtin_signbit(xb[4]) && xb[4] == 0.0 || __builtin_signbit(xb[5]) && xb[5] == 0.0 ||
+        __builtin_signbit(d) && d == 0.0 || __builtin_signbit(de) && de == 0.0) {
+        for (int cu = 0; cu < 2; ++cu) {
+            const double up[2] = {cu == 0 ? d + eps : d + 0.0, cu == 1 ? de + eps : de + 0.0};
+            const double um[2] = {cu == 0 ? d - eps : d + 0.0, cu == 1 ? de - eps : de + 0.0};
+            f_cont(p, xb, up, fp);
+            f_cont(p, xb, um, fm);
+            for (int r = 0; r < 6; ++r) J[4 + cu][r] = (fp[r] - fm[r]) / (2.0 * eps);
         }
     }
-    __syncthreads();
-    // :108  g = x_bar + Ts f - Ad x_bar - Bd u_bar   (f = the rollout's f(x_bar_k, u_prev))
-    for (int it = t; it < 6 * N; it += 64) {
-        const int k = it / 6, r = it % 6;
+    // :106-108  A = I + Ts Jx ; B = Ts Ju ; g = x + Ts f - A x - B u   (f = the rollout's f(x_k, u))
+    double A[36], Bm[12];
+    for (int r = 0; r < 6; ++r) {
+        A[6 * r + 0] = (r == 0 ? 1.0 : 0.0) + Ts * 0.0;
+        A[6 * r + 1] = (r == 1 ? 1.0 : 0.0) + Ts * 0.0;
+        for (int cc = 2; cc < 6; ++cc) A[6 * r + cc] = ((r == cc) ? 1.0 : 0.0) + Ts * J[cc - 2][r];
+        Bm[2 * r + 0] = Ts * J[4][r];
+        Bm[2 * r + 1] = Ts * J[5][r];
+    }
+    const size_t o = (size_t)b * N + k;
+    double* wA = a.wsA + o * 36;
+    double* wB = a.wsB + o * 12;
+    double* wg = a.wsg + o * 6;
+    for (int i = 0; i < 36; ++i) wA[i] = A[i];
+    for (int i = 0; i < 12; ++i) wB[i] = Bm[i];
+    for (int r = 0; r < 6; ++r) {
         double ax = 0.0, bu = 0.0;
-        for (int cc = 0; cc < 6; ++cc) ax += s_A[k * 36 + r * 6 + cc] * s_xbar[6 * k + cc];
-        for (int cc = 0; cc < 2; ++cc) bu += s_B[k * 12 + r * 2 + cc] * s_up[cc];
-        s_g[6 * k + r] = s_xbar[6 * k + r] + Ts * s_fbar[6 * k + r] - ax - bu;
+        for (int cc = 0; cc < 6; ++cc) ax += A[6 * r + cc] * xb[cc];
+        bu += Bm[2 * r] * d;
+        bu += Bm[2 * r + 1] * de;
+        wg[r] = xb[r] + Ts * fb[r] - ax - bu;
     }
-    __syncthreads();
-    // coalesced write-out
-    const size_t o = (size_t)b * N;
-    for (int i = t; i < 36 * N; i += 64) a.wsA[o * 36 + i] = s_A[i];
-    for (int i = t; i < 12 * N; i += 64) a.wsB[o * 12 + i] = s_B[i];
-    for (int i = t; i < 6 * N; i += 64) a.wsg[o * 6 + i] = s_g[i];
 }
 
 }  // namespace tgmpc

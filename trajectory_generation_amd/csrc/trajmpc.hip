@@ -10,6 +10,7 @@
 
 #include "../../include/trajmpc.h"
 #include "mpc_common.h"
+#include "mpc_linearize.h"
 #include "physics.h"
 
 namespace tgmpc {
@@ -159,6 +160,28 @@ __global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, 
 #define TGMPC_DECL(NNV) int launch_mpc_##NNV(const KArgs& a, hipStream_t st, int mode);
 TGMPC_CAPACITIES(TGMPC_DECL)
 #undef TGMPC_DECL
+
+// rollout (one thread per instance) + central-difference linearization (one thread per stage)
+static void launch_linearize(const KArgs& a, hipStream_t st, bool closed) {
+    const int nr = (a.B + 63) / 64, nj = (a.B * a.c.N + 63) / 64;
+    if (closed) {
+        hipLaunchKernelGGL(rollout_kernel<true>, dim3(nr), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(jac_kernel<true>, dim3(nj), dim3(64), 0, st, a);
+    } else {
+        hipLaunchKernelGGL(rollout_kernel<false>, dim3(nr), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(jac_kernel<false>, dim3(nj), dim3(64), 0, st, a);
+    }
+}
+
+// workspace layout: A [B,N,36] | B [B,N,12] | g [B,N,6] | rollout record [B,N,12] | warm [B,4] | order int[B]
+static void carve_workspace(KArgs& a, void* ws, int B, int N) {
+    a.wsA = (double*)ws;
+    a.wsB = a.wsA + (size_t)B * N * 36;
+    a.wsg = a.wsB + (size_t)B * N * 12;
+    a.wsXF = a.wsg + (size_t)B * N * 6;
+    a.wsWarm = a.wsXF + (size_t)B * N * 12;
+    a.Ad = a.wsA; a.Bd = a.wsB; a.gd = a.wsg;
+}
 
 static int launch_mpc(const KArgs& a, hipStream_t st, int mode) {
     const int n = 2 * a.c.N;
@@ -314,23 +337,22 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     a.B = B;
     a.x0 = x0; a.u_prev = u_prev; a.path_ref = path_ref; a.vref = vref;
     if (lin) {
-        a.wsA = (double*)ws;
-        a.wsB = a.wsA + (size_t)B * c->N * 36;
-        a.wsg = a.wsB + (size_t)B * c->N * 12;
-        a.Ad = a.wsA; a.Bd = a.wsB; a.gd = a.wsg;
+        carve_workspace(a, ws, B, c->N);
+        a.wsWarm = nullptr;
     } else {
         a.Ad = Ad; a.Bd = Bd; a.gd = g;
     }
     a.u_cmd = u_cmd; a.status = status; a.objective = objective; a.X_opt = X_opt; a.U_opt = U_opt;
     a.iters = iters; a.polished = polished;
     a.dbg = g_dbg;
+    if (lin) launch_linearize(a, (hipStream_t)stream, false);
     return launch_mpc(a, (hipStream_t)stream, lin ? 0 : 1);
 }
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
     if (B < 0 || N < 0) return 0;
-    // A/B/g hand-off (54 N doubles), warm-start record (4 doubles), closed-loop order (1 int)
-    return ((size_t)B * (size_t)N * 54 + (size_t)B * 4) * sizeof(double) + (((size_t)B * sizeof(int) + 7) & ~(size_t)7);
+    // A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order (1 int)
+    return ((size_t)B * (size_t)N * 66 + (size_t)B * 4) * sizeof(double) + (((size_t)B * sizeof(int) + 7) & ~(size_t)7);
 }
 
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
@@ -391,11 +413,8 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.status = status;
     a.iters = iters;
     a.dbg = g_dbg;
-    a.wsA = (double*)workspace;
-    a.wsB = a.wsA + (size_t)B * c->N * 36;
-    a.wsg = a.wsB + (size_t)B * c->N * 12;
-    a.wsWarm = a.wsg + (size_t)B * c->N * 6;
-    a.Ad = a.wsA; a.Bd = a.wsB; a.gd = a.wsg;
+    carve_workspace(a, workspace, B, c->N);
+    launch_linearize(a, (hipStream_t)stream, true);
     if (t > 0) {
         // order this step's solves by the previous step's iteration counts (longest first)
         int* perm = (int*)(a.wsWarm + (size_t)B * 4);
