@@ -6,8 +6,8 @@
 // Two launches, each with every lane busy:
 //   rollout_kernel  one THREAD per instance runs the serial Euler rollout x_{k+1} = x_k + Ts f(x_k, u)
 //                   (u = u_prev, constant) and records (x_k, f_k) per stage: [B, N, 12].
-//   jac_kernel      one thread per (instance, stage) forms the 6 non-trivial Jacobian columns (phi, vx,
-//                   vy, omega, d, delta) by central differences and writes A_k, B_k, g_k to the
+//   jac_kernel      four threads (one per wave) per (instance, stage) form the 6 non-trivial Jacobian columns (phi,
+//                   vx, vy, omega, d, delta) by central differences and write A_k, B_k, g_k to the
 //                   workspace as [B,N,36], [B,N,12], [B,N,6] (read back by the solve kernel).
 // Columns X, Y are exactly zero (f does not read X, Y: the reference's f(x+dx) - f(x-dx) is 0.0) and
 // are not evaluated.  The difference quotients reuse the parts of f that a perturbation leaves
@@ -89,82 +89,84 @@ __device__ __forceinline__ void f_full(const VP& p, double vx, double vy, double
             long_force(p, vx, d), xd);
 }
 
+// One workgroup = 4 waves x 64 stages: waves 0-2 form the vx / vy / omega columns of their 64
+// stages (a full tire evaluation per side), wave 3 the base tire and the cheap phi / d / delta
+// columns, then assembles A_k, B_k, g_k from the columns staged in LDS (wave-uniform branches).
 template <bool CLOSED>
-__global__ __launch_bounds__(64) void jac_kernel(const KArgs a) {
+__global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
+    __shared__ double sJ[64][6][6];   // [stage in block][column - 2][row]
     const int N = a.c.N;
-    const int idx = blockIdx.x * 64 + threadIdx.x;
-    if (idx >= a.B * N) return;
-    const int b = idx / N, k = idx - b * N;
+    const int s = threadIdx.x & 63, grp = threadIdx.x >> 6;
+    const int gs = blockIdx.x * 64 + s;
+    const bool valid = gs < a.B * N;
+    const int b = valid ? gs / N : 0, k = valid ? gs - b * N : 0;
     const traj_vehicle_params& p = a.p;
     const double Ts = a.c.Ts;
     const double eps = 1e-5;
     const double* rec = a.wsXF + ((size_t)b * N + k) * 12;
     const double* us = CLOSED ? a.u_state + 2 * (size_t)b : a.u_prev + 2 * (size_t)b;
-    double xb[6], fb[6];
-    for (int i = 0; i < 6; ++i) {
-        xb[i] = rec[i];
-        fb[i] = rec[6 + i];
-    }
-    const double d = us[0], de = us[1];
+    double xb[6];
+    for (int i = 0; i < 6; ++i) xb[i] = valid ? rec[i] : 0.0;
+    const double d = valid ? us[0] : 0.0, de = valid ? us[1] : 0.0;
     // unperturbed components as the reference's x + dx carries them (x_i + 0.0)
     const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
     double sphi, cphi, sd, cd;
     sincos(phi, &sphi, &cphi);
     sincos(de, &sd, &cd);
-    const Tire t0 = tire_angles(p, vx, vy, om);
-    const double Ff0 = front_force(p, t0.atf, de), Fr0 = rear_force(p, t0.atr), Fx0 = long_force(p, vx, d);
-
-    double J[6][6];   // J[col - 2][row]
     double fp[6], fm[6];
-    // phi: only sin/cos(phi) change
-    {
-        double sp, cp, sm, cm;
-        sincos(xb[2] + eps, &sp, &cp);
-        sincos(xb[2] - eps, &sm, &cm);
-        f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
-        f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
-        for (int r = 0; r < 6; ++r) J[0][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    }
-    // vx, vy, omega: tire forces recomputed, sin/cos shared
-    {
+    double (*J)[6] = sJ[s];
+    if (grp == 0) {            // vx
         f_full(p, xb[3] + eps, vy, om, sphi, cphi, d, de, sd, cd, fp);
         f_full(p, xb[3] - eps, vy, om, sphi, cphi, d, de, sd, cd, fm);
         for (int r = 0; r < 6; ++r) J[1][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    } else if (grp == 1) {     // vy
         f_full(p, vx, xb[4] + eps, om, sphi, cphi, d, de, sd, cd, fp);
         f_full(p, vx, xb[4] - eps, om, sphi, cphi, d, de, sd, cd, fm);
         for (int r = 0; r < 6; ++r) J[2][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    } else if (grp == 2) {     // omega
         f_full(p, vx, vy, xb[5] + eps, sphi, cphi, d, de, sd, cd, fp);
         f_full(p, vx, vy, xb[5] - eps, sphi, cphi, d, de, sd, cd, fm);
         for (int r = 0; r < 6; ++r) J[3][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    }
-    // d: only the longitudinal force changes
-    {
-        f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d + eps), fp);
-        f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d - eps), fm);
-        for (int r = 0; r < 6; ++r) J[4][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    }
-    // delta: front force and sin/cos(delta) change
-    {
-        double sp, cp, sm, cm;
-        sincos(de + eps, &sp, &cp);
-        sincos(de - eps, &sm, &cm);
-        f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
-        f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
-        for (int r = 0; r < 6; ++r) J[5][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    }
-    // a -0.0 among the components the input columns pass through: evaluate those two columns on the
-    // reference's exact vectors, f(x, u +- du) with u_other + 0.0 (signed zeros then match too)
-    if (__builtin_signbit(xb[2]) && xb[2] == 0.0 || __builtin_signbit(xb[3]) && xb[3] == 0.0 ||
-        __builtin_signbit(xb[4]) && xb[4] == 0.0 || __builtin_signbit(xb[5]) && xb[5] == 0.0 ||
-        __builtin_signbit(d) && d == 0.0 || __builtin_signbit(de) && de == 0.0) {
-        for (int cu = 0; cu < 2; ++cu) {
-            const double up[2] = {cu == 0 ? d + eps : d + 0.0, cu == 1 ? de + eps : de + 0.0};
-            const double um[2] = {cu == 0 ? d - eps : d + 0.0, cu == 1 ? de - eps : de + 0.0};
-            f_cont(p, xb, up, fp);
-            f_cont(p, xb, um, fm);
-            for (int r = 0; r < 6; ++r) J[4 + cu][r] = (fp[r] - fm[r]) / (2.0 * eps);
+    } else {                   // base tire; phi, d, delta
+        const Tire t0 = tire_angles(p, vx, vy, om);
+        const double Ff0 = front_force(p, t0.atf, de), Fr0 = rear_force(p, t0.atr), Fx0 = long_force(p, vx, d);
+        {   // phi: only sin/cos(phi) change
+            double sp, cp, sm, cm;
+            sincos(xb[2] + eps, &sp, &cp);
+            sincos(xb[2] - eps, &sm, &cm);
+            f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
+            f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
+            for (int r = 0; r < 6; ++r) J[0][r] = (fp[r] - fm[r]) / (2.0 * eps);
+        }
+        {   // d: only the longitudinal force changes
+            f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d + eps), fp);
+            f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d - eps), fm);
+            for (int r = 0; r < 6; ++r) J[4][r] = (fp[r] - fm[r]) / (2.0 * eps);
+        }
+        {   // delta: front force and sin/cos(delta) change
+            double sp, cp, sm, cm;
+            sincos(de + eps, &sp, &cp);
+            sincos(de - eps, &sm, &cm);
+            f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
+            f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
+            for (int r = 0; r < 6; ++r) J[5][r] = (fp[r] - fm[r]) / (2.0 * eps);
+        }
+        // a -0.0 among the components the input columns pass through: evaluate those two columns on
+        // the reference's exact vectors, f(x, u +- du) with u_other + 0.0 (signed zeros match too)
+        if ((__builtin_signbit(xb[2]) && xb[2] == 0.0) || (__builtin_signbit(xb[3]) && xb[3] == 0.0) ||
+            (__builtin_signbit(xb[4]) && xb[4] == 0.0) || (__builtin_signbit(xb[5]) && xb[5] == 0.0) ||
+            (__builtin_signbit(d) && d == 0.0) || (__builtin_signbit(de) && de == 0.0)) {
+            for (int cu = 0; cu < 2; ++cu) {
+                const double up[2] = {cu == 0 ? d + eps : d + 0.0, cu == 1 ? de + eps : de + 0.0};
+                const double um[2] = {cu == 0 ? d - eps : d + 0.0, cu == 1 ? de - eps : de + 0.0};
+                f_cont(p, xb, up, fp);
+                f_cont(p, xb, um, fm);
+                for (int r = 0; r < 6; ++r) J[4 + cu][r] = (fp[r] - fm[r]) / (2.0 * eps);
+            }
         }
     }
+    __syncthreads();
+    if (grp != 3 || !valid) return;
     // :106-108  A = I + Ts Jx ; B = Ts Ju ; g = x + Ts f - A x - B u   (f = the rollout's f(x_k, u))
     double A[36], Bm[12];
     for (int r = 0; r < 6; ++r) {
@@ -185,7 +187,7 @@ __global__ __launch_bounds__(64) void jac_kernel(const KArgs a) {
         for (int cc = 0; cc < 6; ++cc) ax += A[6 * r + cc] * xb[cc];
         bu += Bm[2 * r] * d;
         bu += Bm[2 * r + 1] * de;
-        wg[r] = xb[r] + Ts * fb[r] - ax - bu;
+        wg[r] = xb[r] + Ts * rec[6 + r] - ax - bu;
     }
 }
 

@@ -166,10 +166,10 @@ static void launch_linearize(const KArgs& a, hipStream_t st, bool closed) {
     const int nr = (a.B + 63) / 64, nj = (a.B * a.c.N + 63) / 64;
     if (closed) {
         hipLaunchKernelGGL(rollout_kernel<true>, dim3(nr), dim3(64), 0, st, a);
-        hipLaunchKernelGGL(jac_kernel<true>, dim3(nj), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(jac_kernel<true>, dim3(nj), dim3(256), 0, st, a);
     } else {
         hipLaunchKernelGGL(rollout_kernel<false>, dim3(nr), dim3(64), 0, st, a);
-        hipLaunchKernelGGL(jac_kernel<false>, dim3(nj), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(jac_kernel<false>, dim3(nj), dim3(256), 0, st, a);
     }
 }
 
