@@ -1,0 +1,96 @@
+"""KalmanNet on the GPU (trajectory_generation_amd/knet.py + the HIP ops of include/trajknet.h) vs the
+reference's outputs (tests/golden/knet.npz) and the CPU oracle.  float32 throughout, as the reference:
+tolerance 2e-4 x (1 + max|ref|) on normalized posteriors (GEMM summation order and single-precision
+transcendentals differ from the CPU reference; 20 recurrent steps)."""
+import numpy as np
+import pytest
+import torch
+
+from tests._knet_weights import LIMITS, knet_weights
+
+pytestmark = pytest.mark.gpu
+G = np.load("tests/golden/knet.npz")
+
+
+def build(dev, seed=0):
+    from trajectory_generation_amd import knet as K
+    sysm = K.VehicleModel(float(G["Ts"]), 20, 20, torch.zeros(6, 1))
+    sysm.Params.update(LIMITS)
+    model = K.KalmanNetNN(dev)
+    model.NNBuild(sysm, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128)
+    f32 = lambda a: torch.tensor(a, dtype=torch.float32)   # noqa: E731
+    model.set_normalization(f32(G["x_mean"]), f32(G["x_std"]), f32(G["y_mean"]), f32(G["y_std"]))
+    sd = {k: torch.tensor(v) for k, v in knet_weights(seed=seed).items()}
+    model.load_state_dict(sd, strict=True)
+    model.eval()
+    return K, sysm, model
+
+
+def tol(ref):
+    return 2e-4 * (1 + np.abs(ref).max())
+
+
+def test_vehicle_f_h(gpu):
+    K, sysm, _ = build(gpu)
+    x = torch.tensor(G["phys_x"], dtype=torch.float32, device=gpu).unsqueeze(2)
+    u = torch.tensor(G["phys_u"], dtype=torch.float32, device=gpu).unsqueeze(2)
+    out = sysm.f(x, u).squeeze(2).cpu().numpy()
+    np.testing.assert_allclose(out, G["f_step"], rtol=1e-5, atol=1e-5)
+    hh = sysm.h(x).squeeze(2).cpu().numpy()
+    np.testing.assert_array_equal(hh, G["phys_x"][:, [0, 1, 3, 4, 5]].astype(np.float32))
+
+
+def test_missing_limits_raise_like_reference(gpu):
+    from trajectory_generation_amd import knet as K
+    sysm = K.VehicleModel(0.01, 1, 1, torch.zeros(6, 1))
+    x = torch.zeros(2, 6, 1, device=gpu)
+    u = torch.zeros(2, 2, 1, device=gpu)
+    with pytest.raises(KeyError):
+        sysm.f(x, u)
+
+
+def test_sequence_vs_reference(gpu):
+    _, _, model = build(gpu)
+    B, T = G["y_norm"].shape[0], G["y_norm"].shape[2]
+    y = torch.tensor(G["y_norm"], dtype=torch.float32, device=gpu)
+    u = torch.tensor(G["u"], dtype=torch.float32, device=gpu)
+    m1x0 = torch.tensor(G["m1x0"], dtype=torch.float32, device=gpu)
+    with torch.no_grad():
+        model.batch_size = B
+        model.init_hidden_KNet()
+        model.InitSequence(m1x0, T)
+        posts, priors, kgs = [], [], []
+        for t in range(T):
+            posts.append(model(y[:, :, t:t + 1], u[:, :, t:t + 1]).squeeze(2).cpu().numpy())
+            priors.append(model.m1x_prior.squeeze(2).cpu().numpy())
+            kgs.append(model.KGain.cpu().numpy())
+    post, prior, kg = np.stack(posts, 2), np.stack(priors, 2), np.stack(kgs, 3)
+    assert np.abs(prior - G["x_prior"]).max() <= tol(G["x_prior"])
+    assert np.abs(kg - G["KG"]).max() <= tol(G["KG"])
+    assert np.abs(post - G["x_post"]).max() <= tol(G["x_post"])
+    # reference attribute shapes
+    assert model.m1x_posterior.shape == (B, 6, 1) and model.KGain.shape == (B, 6, 5)
+    assert model.h_Q.shape == (1, B, 128) and model.h_Sigma.shape == (1, B, 128) and model.h_S.shape == (1, B, 128)
+
+
+def test_graph_runner_matches_eager_and_oracle(gpu):
+    from oracle import knet_oracle as KO
+    from trajectory_generation_amd.knet import KNetSequenceRunner
+    _, sysm, model = build(gpu)
+    rng = np.random.default_rng(5)
+    B, T = 64, 30
+    y = torch.tensor(rng.normal(size=(B, 5, T)), dtype=torch.float32, device=gpu)
+    u = torch.tensor(np.stack([rng.uniform(0, 0.5, (B, T)), rng.uniform(-0.3, 0.3, (B, T))], 1), dtype=torch.float32,
+                     device=gpu)
+    m1x0 = torch.tensor(rng.normal(size=(B, 6, 1)) * 0.5, dtype=torch.float32, device=gpu)
+    run = KNetSequenceRunner(model, B)
+    eager = run.run(y, u, m1x0, use_graph=False).cpu().numpy()
+    g1 = run.run(y, u, m1x0, use_graph=True).cpu().numpy()
+    g2 = run.run(y, u, m1x0, use_graph=True).cpu().numpy()    # replay of the captured graph
+    np.testing.assert_array_equal(g1, eager)
+    np.testing.assert_array_equal(g2, eager)
+    p = dict(KO.PARAMS)
+    p.update(LIMITS)
+    ref = KO.run_sequences(knet_weights(0), p, float(G["Ts"]), y.cpu().numpy(), u.cpu().numpy(), m1x0.cpu().numpy(),
+                           G["x_mean"], G["x_std"], G["y_mean"], G["y_std"]).numpy()
+    assert np.abs(eager - ref).max() <= 1e-3 * (1 + np.abs(ref).max())

@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtrajmpc.so")
 CSRC = os.path.join(_HERE, "csrc")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "trajmpc.h")
+HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "trajknet.h")]
 
 TRAJ_OK, TRAJ_E_ARG, TRAJ_E_UNSUPPORTED, TRAJ_E_LAUNCH = 0, -1, -2, -3
 MAX_N = 40
@@ -59,6 +60,13 @@ class MpcConfig(C.Structure):
     ]
 
 
+class KnetLimits(C.Structure):
+    """traj_knet_limits (state clamp limits of vehicle_model.py:54-57,125-131)."""
+    _fields_ = [(k, C.c_float) for k in (
+        "x_min", "x_max", "y_min", "y_max", "phi_min", "phi_max", "vx_min", "vx_max", "vy_min", "vy_max",
+        "omega_min", "omega_max")]
+
+
 class Paths(C.Structure):
     """traj_paths (closed-loop reference geometry per trajectory)."""
     _fields_ = [("kmax", C.c_int), ("kind", _V), ("pc", _V), ("nk", _V), ("xk", _V), ("coef", _V)]
@@ -85,6 +93,10 @@ _SIGS = {
                                     _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_ref_window_batch": (C.c_int, [C.POINTER(Paths), C.c_int, C.c_int, C.c_double, _V, _V, _V, _V]),
     "traj_debug_set_stamps": (C.c_int, [_V]),
+    "traj_knet_prior_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float, C.c_int,
+                                      _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "traj_knet_gru_gates_f32": (C.c_int, [C.c_int, C.c_int, _V, _V, _V, _V, _V]),
+    "traj_knet_update_f32": (C.c_int, [C.c_int, _V, _V, _V, _V, _V, _V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,
                                         _V, _V, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V, C.c_size_t, _V]),
 }

@@ -1,0 +1,318 @@
+"""KalmanNet inference on MI355X: drop-in for KalmanNet/kalman_net.py (KalmanNetNN) and
+KalmanNet/vehicle_model.py (VehicleModel), float32 like the reference.
+
+Same class names, constructor/NNBuild arguments, attributes (``batch_size``, ``m1x_posterior``,
+``h_Q`` / ``h_Sigma`` / ``h_S``, ``KGain``, ``f`` / ``h``) and ``state_dict`` keys as the reference, so
+its checkpoints load unchanged.  What runs on the device per step (kalman_net.py:169-216):
+
+* ``traj_knet_prior_f32``   (HIP) denormalize, vehicle f (clamped Euler step), h, renormalize, and the
+  innovation y - m1y: kalman_net.py:145-162 in one kernel;
+* the gain network's dense layers as library GEMMs (``torch.addmm`` -> hipBLASLt), ReLU in place;
+* ``traj_knet_gru_gates_f32`` (HIP) the three GRU cells' gate arithmetic after their two GEMMs;
+* ``traj_knet_update_f32`` (HIP) x_post = x_prior + sigmoid(innov_logit) * KG dy (:169-178).
+
+``KNetSequenceRunner`` captures one whole step in a HIP graph and replays it T times.
+There is no CPU path: the ops raise without the HIP library or a GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from .batch import REFERENCE_PARAMS, params_struct, require_gpu
+
+Params = dict(REFERENCE_PARAMS)
+
+LIMIT_KEYS = ("x_min", "x_max", "y_min", "y_max", "phi_min", "phi_max", "vx_min", "vx_max", "vy_min", "vy_max",
+              "omega_min", "omega_max")
+
+
+def _p(t):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def limits_struct(params: dict) -> _lib.KnetLimits:
+    missing = [k for k in LIMIT_KEYS if k not in params]
+    if missing:
+        # vehicle_model.py:54 reads p["phi_min"] etc.; the reference raises KeyError without them
+        raise KeyError(missing[0])
+    s = _lib.KnetLimits()
+    for k in LIMIT_KEYS:
+        setattr(s, k, float(params[k]))
+    return s
+
+
+def knet_prior(params: dict, Ts: float, x_post, u, x_mean, x_std, y_mean, y_std, y=None, u_mean=None, u_std=None):
+    """kalman_net.py:145-162 for B sequences: returns (m1x_prior [B,6], m1y [B,5], dy [B,5] or None)."""
+    dev = x_post.device
+    B = x_post.shape[0]
+    xp = x_post.reshape(B, 6).contiguous()
+    uu = u.reshape(B, 2).contiguous()
+    yy = None if y is None else y.reshape(B, 5).contiguous()
+    prior = torch.empty((B, 6), dtype=torch.float32, device=dev)
+    m1y = torch.empty((B, 5), dtype=torch.float32, device=dev)
+    dy = None if y is None else torch.empty((B, 5), dtype=torch.float32, device=dev)
+    flat = lambda t: None if t is None else t.reshape(-1).contiguous()   # noqa: E731
+    _lib.check(_lib.lib().traj_knet_prior_f32(
+        C.byref(params_struct(params)), C.byref(limits_struct(params)), float(Ts), B, _p(xp), _p(uu), _p(yy),
+        _p(flat(x_mean)), _p(flat(x_std)), _p(flat(y_mean)), _p(flat(y_std)), _p(flat(u_mean)), _p(flat(u_std)),
+        _p(prior), _p(m1y), _p(dy), _stream()), "traj_knet_prior_f32")
+    return prior, m1y, dy
+
+
+def gru_cell(x, h, gru: nn.GRU):
+    """One step of a 1-layer torch.nn.GRU: two GEMMs + the fused gate kernel. x [B,in], h [B,H]."""
+    gi = torch.addmm(gru.bias_ih_l0, x, gru.weight_ih_l0.t())
+    gh = torch.addmm(gru.bias_hh_l0, h, gru.weight_hh_l0.t())
+    out = torch.empty_like(h)
+    B, H = h.shape
+    _lib.check(_lib.lib().traj_knet_gru_gates_f32(B, H, _p(gi), _p(gh), _p(h), _p(out), _stream()),
+               "traj_knet_gru_gates_f32")
+    return out
+
+
+def _linear(x, lin: nn.Linear, relu: bool):
+    y = torch.addmm(lin.bias, x, lin.weight.t())
+    return F.relu_(y) if relu else y
+
+
+class VehicleModel:
+    """vehicle_model.py:81-153.  ``Params`` must carry the 12 clamp limits (``LIMIT_KEYS``)."""
+
+    def __init__(self, Ts, T_train, T_test, m1x_0_real, prior_Q=None, prior_Sigma=None, prior_S=None):
+        self.m, self.n, self.d = 6, 5, 2
+        self.Ts = Ts
+        self.Params = dict(Params)
+        self.T, self.T_test = T_train, T_test
+        self.m1x_0 = m1x_0_real
+        self.prior_Q, self.prior_Sigma, self.prior_S = prior_Q, prior_Sigma, prior_S
+
+    def f(self, x_batch_in, u_batch_in):
+        """x [B,6,1], u [B,2,1] -> clamped Euler step [B,6,1] (vehicle_model.py:109-134)."""
+        dev = x_batch_in.device
+        one6 = torch.ones(6, dtype=torch.float32, device=dev)
+        one5 = torch.ones(5, dtype=torch.float32, device=dev)
+        prior, _, _ = knet_prior(self.Params, self.Ts, x_batch_in.float(), u_batch_in.float(),
+                                 torch.zeros_like(one6), one6, torch.zeros_like(one5), one5)
+        return prior.unsqueeze(2)
+
+    def h(self, x_batch_in):
+        """rows X, Y, vx, vy, omega (vehicle_model.py:136-153)."""
+        idx = torch.tensor([0, 1, 3, 4, 5], device=x_batch_in.device)
+        return torch.index_select(x_batch_in, 1, idx)
+
+
+class KalmanNetNN(nn.Module):
+    """kalman_net.py:5-223 with the step fused on the device (see the module docstring)."""
+
+    def __init__(self, device=None):
+        super().__init__()
+        self.device = require_gpu(device)
+        self.has_norm_params_xy = False
+        self.has_norm_params_u = False
+        self.u_mean = self.u_std = None
+
+    def set_normalization(self, x_mean, x_std, y_mean, y_std, u_mean=None, u_std=None):
+        self.x_mean = x_mean.to(self.device, torch.float32)
+        self.x_std = x_std.to(self.device, torch.float32)
+        self.y_mean = y_mean.to(self.device, torch.float32)
+        self.y_std = y_std.to(self.device, torch.float32)
+        self.has_norm_params_xy = True
+        if (u_mean is not None) and (u_std is not None):
+            self.u_mean = u_mean.to(self.device, torch.float32)
+            self.u_std = u_std.to(self.device, torch.float32)
+            self.has_norm_params_u = True
+        else:
+            self.u_mean = self.u_std = None
+            self.has_norm_params_u = False
+
+    def NNBuild(self, SysModel, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128):
+        """kalman_net.py:26-113: the same modules, shapes and names (state_dict compatible)."""
+        self.innov_logit = nn.Parameter(torch.tensor(0.0))
+        self.sys = SysModel
+        self.f = SysModel.f
+        self.h = SysModel.h
+        self.m = SysModel.m
+        self.n = SysModel.n
+        self.seq_len_input = 1
+        self.batch_size = 0
+        m, n, H = self.m, self.n, hidden_dim_gru
+        self.d_input_FC5, self.d_output_FC5 = m, m * in_mult_KNet
+        self.FC5 = nn.Sequential(nn.Linear(m, m * in_mult_KNet), nn.ReLU(), nn.Dropout(p=0.05))
+        self.d_input_Q, self.d_hidden_Q = self.d_output_FC5, H
+        self.GRU_Q = nn.GRU(self.d_input_Q, H)
+        self.d_input_Sigma, self.d_hidden_Sigma = H, H
+        self.GRU_Sigma = nn.GRU(H, H)
+        self.d_input_FC1, self.d_output_FC1 = H, n * n
+        self.FC1 = nn.Sequential(nn.Linear(H, n * n), nn.ReLU(), nn.Dropout(p=0.05))
+        self.d_input_FC7, self.d_output_FC7 = n, n
+        self.FC7 = nn.Sequential(nn.Linear(n, n), nn.ReLU(), nn.Dropout(p=0.05))
+        self.d_input_S, self.d_hidden_S = n * n + n, H
+        self.GRU_S = nn.GRU(self.d_input_S, H)
+        self.d_input_FC2 = 2 * H
+        self.d_output_FC2 = n * m
+        self.d_hidden_FC2 = self.d_input_FC2 * out_mult_KNet
+        self.FC2 = nn.Sequential(nn.Linear(self.d_input_FC2, self.d_hidden_FC2), nn.ReLU(),
+                                 nn.Linear(self.d_hidden_FC2, self.d_output_FC2), nn.Dropout(p=0.1))
+        self.d_input_FC3, self.d_output_FC3 = H + n * m, m * m
+        self.FC3 = nn.Sequential(nn.Linear(self.d_input_FC3, m * m), nn.ReLU(), nn.Dropout(p=0.05))
+        self.d_input_FC4, self.d_output_FC4 = H + m * m, H
+        self.FC4 = nn.Sequential(nn.Linear(self.d_input_FC4, H), nn.ReLU(), nn.Dropout(p=0.05))
+        self.to(self.device)
+
+    # ---------- normalization bridge (kalman_net.py:119-143) ----------
+    def _denorm_x(self, x_norm):
+        return x_norm * self.x_std + self.x_mean if self.has_norm_params_xy else x_norm
+
+    def _renorm_x(self, x_real):
+        return (x_real - self.x_mean) / self.x_std if self.has_norm_params_xy else x_real
+
+    def _denorm_y(self, y_norm):
+        return y_norm * self.y_std + self.y_mean if self.has_norm_params_xy else y_norm
+
+    def _renorm_y(self, y_real):
+        return (y_real - self.y_mean) / self.y_std if self.has_norm_params_xy else y_real
+
+    def _denorm_u(self, u_in):
+        return u_in * self.u_std + self.u_mean if self.has_norm_params_u else u_in
+
+    def _norm_tensors(self):
+        if self.has_norm_params_xy:
+            return self.x_mean, self.x_std, self.y_mean, self.y_std
+        dev = self.device
+        return (torch.zeros(6, device=dev), torch.ones(6, device=dev), torch.zeros(5, device=dev),
+                torch.ones(5, device=dev))
+
+    def InitSequence(self, M1_0_norm, T):
+        self.T = T
+        self.m1x_posterior = M1_0_norm.to(self.device, torch.float32)
+
+    def init_hidden_KNet(self):
+        B, dev = self.batch_size, self.device
+        self.h_S = torch.zeros((self.seq_len_input, B, self.d_hidden_S), device=dev)
+        self.h_Sigma = torch.zeros((self.seq_len_input, B, self.d_hidden_Sigma), device=dev)
+        self.h_Q = torch.zeros((self.seq_len_input, B, self.d_hidden_Q), device=dev)
+
+    # ---------- one step ----------
+    def step_prior(self, u, y=None):
+        xm, xs, ym, ys = self._norm_tensors()
+        prior, m1y, dy = knet_prior(self.sys.Params, self.sys.Ts, self.m1x_posterior, u, xm, xs, ym, ys, y=y,
+                                    u_mean=self.u_mean, u_std=self.u_std)
+        self.m1x_prior = prior.unsqueeze(2)
+        self.m1y = m1y.unsqueeze(2)
+        return dy
+
+    def KGain_step(self, obs_innov_diff, m1x_prior):
+        """kalman_net.py:180-212: x [B,n] innovation, [B,m] prior -> FC2 output [B, n*m]."""
+        drop = self.training
+        def dp(x, mod):   # noqa: E306  (Dropout modules: identity in eval mode)
+            return mod(x) if drop else x
+        B = m1x_prior.shape[0]
+        out_FC5 = dp(_linear(m1x_prior, self.FC5[0], True), self.FC5[2])
+        h_Q = gru_cell(out_FC5, self.h_Q.reshape(B, -1), self.GRU_Q)
+        out_Sigma = gru_cell(h_Q, self.h_Sigma.reshape(B, -1), self.GRU_Sigma)
+        out_FC1 = dp(_linear(out_Sigma, self.FC1[0], True), self.FC1[2])
+        out_FC7 = dp(_linear(obs_innov_diff, self.FC7[0], True), self.FC7[2])
+        h_S = gru_cell(torch.cat((out_FC1, out_FC7), 1), self.h_S.reshape(B, -1), self.GRU_S)
+        hid = _linear(torch.cat((out_Sigma, h_S), 1), self.FC2[0], True)
+        out_FC2 = dp(_linear(hid, self.FC2[2], False), self.FC2[3])
+        out_FC3 = dp(_linear(torch.cat((h_S, out_FC2), 1), self.FC3[0], True), self.FC3[2])
+        out_FC4 = dp(_linear(torch.cat((out_Sigma, out_FC3), 1), self.FC4[0], True), self.FC4[2])
+        self.h_Q = h_Q.unsqueeze(0)
+        self.h_S = h_S.unsqueeze(0)
+        self.h_Sigma = out_FC4.unsqueeze(0)
+        return out_FC2
+
+    def KNet_step(self, y, u):
+        B = y.shape[0]
+        dy = self.step_prior(u, y=y)
+        KG = self.KGain_step(dy, self.m1x_prior.reshape(B, self.m))
+        self.KGain = KG.reshape(self.batch_size, self.m, self.n)
+        post = torch.empty((B, self.m), dtype=torch.float32, device=self.device)
+        _lib.check(_lib.lib().traj_knet_update_f32(B, _p(self.m1x_prior.reshape(B, self.m).contiguous()),
+                                                   _p(KG.contiguous()), _p(dy), _p(self.innov_logit.detach()),
+                                                   _p(post), _stream()), "traj_knet_update_f32")
+        self.m1x_posterior = post.unsqueeze(2)
+        return self.m1x_posterior
+
+    def forward(self, y, u):
+        """y [B,n,1] normalized, u [B,m_u,1] -> normalized posterior [B,m,1] (kalman_net.py:214-216)."""
+        return self.KNet_step(y.to(self.device, torch.float32), u.to(self.device, torch.float32))
+
+
+class KNetSequenceRunner:
+    """T steps of a KalmanNetNN (eval mode) for B sequences, one step captured in a HIP graph.
+
+    Mirrors the inference loop of training_prediction.py:118-137 / test_vehicle.py:123-145:
+    init_hidden_KNet, InitSequence(m1x0), then forward(y[:, :, t], u[:, :, t]) for t < T."""
+
+    def __init__(self, model: KalmanNetNN, B: int):
+        self.model, self.B = model, B
+        dev = model.device
+        self.y = torch.zeros((B, model.n, 1), device=dev)
+        self.u = torch.zeros((B, 2, 1), device=dev)
+        self.graph = None
+
+    def _init_state(self, m1x0):
+        md = self.model
+        md.batch_size = self.B
+        md.init_hidden_KNet()
+        md.InitSequence(m1x0, 0)
+
+    @torch.no_grad()
+    def run(self, y_seq, u_seq, m1x0, use_graph=True):
+        """y_seq [B,n,T] normalized, u_seq [B,2,T], m1x0 [B,m,1] -> posterior [B,m,T] (normalized)."""
+        md = self.model
+        T = y_seq.shape[2]
+        out = torch.empty((self.B, md.m, T), device=md.device)
+        if not use_graph:
+            self._init_state(m1x0)
+            for t in range(T):
+                out[:, :, t] = md(y_seq[:, :, t:t + 1], u_seq[:, :, t:t + 1]).squeeze(2)
+            return out
+        # static-buffer form of the step for capture: the module's state tensors are updated in place
+        self._init_state(m1x0)
+        state = {"post": md.m1x_posterior.clone(), "hQ": md.h_Q.clone(), "hS": md.h_S.clone(),
+                 "hSig": md.h_Sigma.clone()}
+
+        def step():
+            md.m1x_posterior, md.h_Q, md.h_S, md.h_Sigma = state["post"], state["hQ"], state["hS"], state["hSig"]
+            r = md(self.y, self.u)
+            state["post"].copy_(r)
+            state["hQ"].copy_(md.h_Q)
+            state["hS"].copy_(md.h_S)
+            state["hSig"].copy_(md.h_Sigma)
+
+        if self.graph is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):   # warm up the library GEMM paths before capture
+                    step()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            self.graph, self.state = g, state
+        else:
+            state = self.state
+        # (re)initialize the captured state buffers
+        self._init_state(m1x0)
+        state["post"].copy_(md.m1x_posterior)
+        state["hQ"].zero_()
+        state["hS"].zero_()
+        state["hSig"].zero_()
+        for t in range(T):
+            self.y.copy_(y_seq[:, :, t:t + 1])
+            self.u.copy_(u_seq[:, :, t:t + 1])
+            self.graph.replay()
+            out[:, :, t] = state["post"].squeeze(2)
+        return out
