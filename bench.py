@@ -65,6 +65,61 @@ def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):
                        f"{dt:.2f} s")
 
 
+# KalmanNet (BASELINE.json configs[4]): 1024 sequences x 200 steps, Ts = 0.01, float32
+KNET_FLOP_PER_SEQ_STEP = 2 * 3_178_373     # MACs of one gain-network step x 2
+FP32_MFMA_PEAK_TFS = 157.3                 # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+KNET_LIMITS = {"x_min": -5.0, "x_max": 40.0, "y_min": -6.0, "y_max": 6.0, "phi_min": -3.2, "phi_max": 3.2,
+               "vx_min": 0.0, "vx_max": 3.0, "vy_min": -1.0, "vy_max": 1.0, "omega_min": -6.0, "omega_max": 6.0}
+
+
+def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50):
+    """Sequences/s of KalmanNet inference (random-init weights of the reference architecture,
+    synthetic normalized inputs resident on the GPU), one step replayed as a HIP graph."""
+    from trajectory_generation_amd import knet as K
+    torch.manual_seed(0)
+    sysm = K.VehicleModel(0.01, T, T, torch.zeros(6, 1))
+    sysm.Params.update(KNET_LIMITS)
+    model = K.KalmanNetNN(dev)
+    model.NNBuild(sysm, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128)
+    model.set_normalization(torch.zeros(1, 6, 1), torch.ones(1, 6, 1), torch.zeros(1, 5, 1), torch.ones(1, 5, 1))
+    model.eval()
+    g = torch.Generator(device="cpu").manual_seed(1)
+    y = torch.randn((B, 5, T), generator=g).to(dev)
+    u = (0.2 * torch.randn((B, 2, T), generator=g)).to(dev)
+    m1x0 = (0.5 * torch.randn((B, 6, 1), generator=g)).to(dev)
+    run = K.KNetSequenceRunner(model, B)
+    run.run(y, u, m1x0)                  # capture + warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run.run(y, u, m1x0)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    achieved = KNET_FLOP_PER_SEQ_STEP * B * T / dt / 1e12
+    out = {"metric": f"KalmanNet seq/s (B={B}, T={T})", "value": B / dt, "unit": "sequences/s",
+           "ms_per_step": 1e3 * dt / T, "dtype": "f32",
+           "config": {"workload": "KalmanNetNN inference (in_mult 5, out_mult 40, hidden 128), random-init weights, "
+                                  "synthetic normalized inputs", "batch": B, "T": T, "Ts": 0.01},
+           "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": achieved / FP32_MFMA_PEAK_TFS, "traffic": None,
+                        "flop_per_seq_step": KNET_FLOP_PER_SEQ_STEP}}
+    if cpu:
+        import oracle.knet_oracle as KO  # test infrastructure: CPU-baseline leg only
+        w = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        p = dict(KO.PARAMS)
+        p.update(KNET_LIMITS)
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        z6, o6, z5, o5 = np.zeros((1, 6, 1)), np.ones((1, 6, 1)), np.zeros((1, 5, 1)), np.ones((1, 5, 1))
+        t0 = time.perf_counter()
+        KO.run_sequences(w, p, 0.01, y[:, :, :cpu_T].cpu().numpy(), u[:, :, :cpu_T].cpu().numpy(),
+                         m1x0.cpu().numpy(), z6, o6, z5, o5)
+        dtc = (time.perf_counter() - t0) * (T / cpu_T)
+        out["cpu_baseline"] = {"value": B / dtc, "unit": "sequences/s", "cores": threads, "kind": "port",
+                               "sample": f"{B} sequences x {cpu_T} steps (scaled to T={T}), oracle/knet_oracle.py "
+                                         f"(torch CPU float32, {threads} threads)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +133,7 @@ def main():
     ap.add_argument("--cpu-traj", type=int, default=4096)
     ap.add_argument("--cpu-steps", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-knet", action="store_true", help="skip the KalmanNet measurement (configs[4])")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
     args = ap.parse_args()
@@ -182,6 +238,8 @@ def main():
                                            cfg.warm_start)
     else:
         out["cpu_baseline"] = None
+    if not args.no_knet and world == 1:
+        out["knet"] = knet_measure(dev, cpu=not args.no_cpu)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -370,3 +370,22 @@ def test_state_bounds_fail_loudly(gpu):
     x0, up, pr, vr = random_instances(14, 1, 20, 0.05)
     with pytest.raises(NotImplementedError):
         M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, x_lo=[-1e3] * 6)
+
+
+# ------------------------------------------------------------------ dataset emitter (f1)
+
+def test_dataset_generate_single_rank(gpu, tmp_path):
+    import pandas as pd
+    from trajectory_generation_amd import dataset as D
+    from trajectory_generation_amd.workload import make_workload
+    B, T, N, Ts = 6, 8, 20, 0.05
+    X, U, st = D.generate(B, T, N=N, Ts=Ts, kind="spline", seed=1, out_prefix=str(tmp_path / "ds"))
+    w = make_workload(B, N, Ts, kind="spline", seed=1)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts))
+    assert torch.equal(X, res["X"]) and torch.equal(U, res["U"])
+    assert st.shape == (B, T)
+    clean = pd.read_csv(tmp_path / "ds_clean.csv", float_precision="round_trip")
+    noisy = pd.read_csv(tmp_path / "ds_noisy.csv", float_precision="round_trip")
+    assert len(clean) == B * (T + 1) and list(noisy.columns)[-1] == "trajectory_id"
+    np.testing.assert_allclose(clean["phi"].to_numpy().reshape(B, T + 1), X[:, :, 2].cpu().numpy(), rtol=0, atol=0)

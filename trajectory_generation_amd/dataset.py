@@ -1,0 +1,97 @@
+"""Closed-loop trajectory dataset emitter and its multi-GPU gather (8(e)).
+
+B trajectories per rank run the device-resident closed loop (batch.run_closed_loop: MPC/main.py:85-101
+for every trajectory), then the histories are written in the reference's dataset schema
+(generation_traj/generation_type1.py:139-158, :295-339):
+
+  clean CSV  t, X, Y, phi, vx, vy, omega, d, delta, trajectory_id
+  noisy CSV  t, X, Y, vx, vy, omega, d, delta, trajectory_id        (phi not measured)
+
+one row per time step (T+1 rows per trajectory, the last row's d / delta = NaN), measurement noise
+drawn exactly as the reference draws it: ``numpy.random.default_rng(12345 + trajectory_id)``, one
+``normal(0, std, T+1)`` vector per channel in the order X, Y, phi, vx, vy, omega (ControlRules,
+generation_type1.py:19-33, :312-322).  These files feed merge_datasets.py / data_loader.py unchanged.
+
+Sharding: rank r owns trajectory ids [r B, (r+1) B) (ids and per-trajectory seeds are global, so the
+result does not depend on the rank count); the only collective is the final gather of the histories
+to rank 0 over RCCL (all_gather of fixed-size per-rank blocks), after which rank 0 writes the CSVs.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+MEAS_NOISE_STD = {"X": 0.05, "Y": 0.05, "phi": 0.003, "vx": 0.010, "vy": 0.003, "omega": 0.030}
+NOISE_SEED_BASE = 12345
+CLEAN_COLUMNS = ["t", "X", "Y", "phi", "vx", "vy", "omega", "d", "delta", "trajectory_id"]
+NOISY_COLUMNS = ["t", "X", "Y", "vx", "vy", "omega", "d", "delta", "trajectory_id"]
+
+
+def measurement_noise(traj_id: int, n_rows: int, stds=None, seed_base=NOISE_SEED_BASE) -> np.ndarray:
+    """[n_rows, 6] noise of one trajectory, generation_type1.py:312-320."""
+    s = MEAS_NOISE_STD if stds is None else stds
+    rng = np.random.default_rng(seed_base + int(traj_id))
+    return np.column_stack([rng.normal(0, s[k], n_rows) for k in ("X", "Y", "phi", "vx", "vy", "omega")])
+
+
+def frames(X, U, ids, Ts):
+    """X [B,T+1,6], U [B,T,2] (numpy), ids [B] -> (clean, noisy) pandas DataFrames in the reference
+    column order, trajectories stacked in id order."""
+    import pandas as pd
+    X = np.asarray(X, dtype=np.float64)
+    U = np.asarray(U, dtype=np.float64)
+    B, n_rows = X.shape[0], X.shape[1]
+    t = np.arange(n_rows) * Ts
+    Xn = X + np.stack([measurement_noise(i, n_rows) for i in ids])
+    dU = np.concatenate([U, np.full((B, 1, 2), np.nan)], axis=1)
+    tid = np.repeat(np.asarray(ids, dtype=np.int64), n_rows)
+    tt = np.tile(t, B)
+
+    def cols(S, with_phi):
+        d = {"t": tt, "X": S[:, :, 0].ravel(), "Y": S[:, :, 1].ravel()}
+        if with_phi:
+            d["phi"] = S[:, :, 2].ravel()
+        d.update({"vx": S[:, :, 3].ravel(), "vy": S[:, :, 4].ravel(), "omega": S[:, :, 5].ravel(),
+                  "d": dU[:, :, 0].ravel(), "delta": dU[:, :, 1].ravel(), "trajectory_id": tid})
+        return pd.DataFrame(d)
+
+    return cols(X, True)[CLEAN_COLUMNS], cols(Xn, False)[NOISY_COLUMNS]
+
+
+def gather_histories(X, U, dist=None):
+    """Concatenate the per-rank [B,T+1,6] / [B,T,2] blocks on every rank (rank order = id order)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return X, U
+    import torch
+    W = dist.get_world_size()
+    outX = torch.empty((W * X.shape[0],) + tuple(X.shape[1:]), dtype=X.dtype, device=X.device)
+    outU = torch.empty((W * U.shape[0],) + tuple(U.shape[1:]), dtype=U.dtype, device=U.device)
+    dist.all_gather_into_tensor(outX, X.contiguous())
+    dist.all_gather_into_tensor(outU, U.contiguous())
+    return outX, outU
+
+
+def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=None, polish_mode=0):
+    """Run the closed loop for this rank's B trajectories, gather to every rank and (rank 0) write
+    ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv``.  Returns (X, U, status) for all ranks."""
+    import torch
+    from . import batch as TB
+    from .workload import make_workload
+    rank = dist.get_rank() if (dist is not None and dist.is_initialized()) else 0
+    w = make_workload(B, N, Ts, kind=kind, seed=seed, id_offset=rank * B)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode))
+    X, U = gather_histories(res["X"], res["U"], dist)
+    st = res["status"]
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        allst = torch.empty((dist.get_world_size() * st.shape[0],) + tuple(st.shape[1:]), dtype=st.dtype,
+                            device=st.device)
+        dist.all_gather_into_tensor(allst, st.t().contiguous())
+        st = allst
+    else:
+        st = st.t()
+    if out_prefix is not None and rank == 0:
+        ids = np.arange(X.shape[0])
+        clean, noisy = frames(X.cpu().numpy(), U.cpu().numpy(), ids, Ts)
+        clean.to_csv(f"{out_prefix}_clean.csv", index=False)
+        noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
+    return X, U, st
