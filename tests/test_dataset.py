@@ -76,3 +76,20 @@ def test_gather_two_ranks_gloo():
     assert gX.shape == (8, 7, 6) and gU.shape == (8, 6, 2)
     np.testing.assert_array_equal(gX[:, 0, 0], np.arange(8))      # rank order == global id order
     np.testing.assert_array_equal(gU[:, 0, 0], -np.arange(8))
+
+
+def test_loader_matches_reference(tmp_path):
+    """dataset.load_vehicle_dataset vs the reference's data_loader.py on the same CSVs (tests/golden/loader.npz)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from gen_loader_golden import synthetic_histories
+    X, U, Ts = synthetic_histories()
+    clean, noisy = D.frames(X, U, np.arange(X.shape[0]), Ts)
+    clean.to_csv(tmp_path / "c.csv", index=False)
+    noisy.to_csv(tmp_path / "n.csv", index=False)
+    got = D.load_vehicle_dataset(tmp_path / "n.csv", tmp_path / "c.csv", T_steps=25)
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "loader.npz"))
+    for name, part in zip(("train", "val", "test"), got):
+        for k, t in zip("yux", part):
+            np.testing.assert_array_equal(t.numpy(), g[f"{name}_{k}"])
+    assert D.load_vehicle_dataset(tmp_path / "missing.csv", tmp_path / "c.csv") is None

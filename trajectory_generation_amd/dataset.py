@@ -95,3 +95,46 @@ def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=N
         clean.to_csv(f"{out_prefix}_clean.csv", index=False)
         noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
     return X, U, st
+
+
+def load_vehicle_dataset(noisy_csv_path, clean_csv_path, T_steps=600, train_split=0.7, val_split=0.15, seed=42,
+                         device=None):
+    """KalmanNet/data_loader.py:5-109 (load_vehicle_dataset), vectorized: the first T_steps rows of every
+    trajectory (ids 0..n-1), y = noisy [X, Y, vx, vy, omega], u = [d, delta], x = clean
+    [X, Y, phi, vx, vy, omega] as float32 [n, C, T]; trajectories shuffled by default_rng(seed) and split
+    70 / 15 / 15.  Returns ((y, u, x) train, val, test) torch tensors (on ``device`` if given), or None
+    when a file or a trajectory is missing, as the reference does."""
+    import pandas as pd
+    import torch
+    try:
+        dn = pd.read_csv(noisy_csv_path)
+        dc = pd.read_csv(clean_csv_path)
+    except FileNotFoundError:
+        return None
+    n = dn["trajectory_id"].nunique()
+
+    def block(df, cols):
+        df = df[df["trajectory_id"] < n]
+        df = df.assign(_r=df.groupby("trajectory_id").cumcount())
+        df = df[df["_r"] < T_steps]
+        counts = df.groupby("trajectory_id").size()
+        if len(counts) != n or (counts < T_steps).any():
+            raise KeyError("trajectory missing or shorter than T_steps")
+        df = df.sort_values(["trajectory_id", "_r"], kind="stable")
+        return df[cols].to_numpy(dtype=np.float32).reshape(n, T_steps, len(cols)).transpose(0, 2, 1)
+
+    try:
+        y = block(dn, ["X", "Y", "vx", "vy", "omega"])
+        u = block(dn, ["d", "delta"])
+        x = block(dc, ["X", "Y", "phi", "vx", "vy", "omega"])
+    except KeyError:
+        return None
+    idx = np.arange(n)
+    np.random.default_rng(seed).shuffle(idx)
+    y, u, x = y[idx], u[idx], x[idx]
+    n_tr, n_va = int(n * train_split), int(n * val_split)
+    cut = lambda a: (a[:n_tr], a[n_tr:n_tr + n_va], a[n_tr + n_va:])   # noqa: E731
+    out = []
+    for part in zip(cut(y), cut(u), cut(x)):
+        out.append(tuple(torch.tensor(np.ascontiguousarray(p), dtype=torch.float32, device=device) for p in part))
+    return tuple(out)
