@@ -11,6 +11,7 @@
  *   vehicle_model.py:19-79,109-153 f (clamps, Euler), h     kalman_net.py:161-162)
  *   torch.nn.GRU cell (seq_len 1), gates r, z, n            traj_knet_gru_gates_f32
  *   kalman_net.py:169-178 KNet_step posterior update        traj_knet_update_f32
+ *   (no reference counterpart) EKF baseline of config 5     traj_ekf_run_f64
  *
  * Conventions as trajmpc.h: device pointers, row-major, asynchronous on `stream`, 0 / TRAJ_E_*.
  */
@@ -53,6 +54,19 @@ int traj_knet_gru_gates_f32(int B, int H, const float* gi, const float* gh, cons
  * KG [B,6,5] row-major (the reshape of FC2's output), dy [B,5], innov_logit: device scalar. */
 int traj_knet_update_f32(int B, const float* x_prior, const float* KG, const float* dy, const float* innov_logit,
                          float* x_post, void* stream);
+
+/* Build-defined EKF baseline for config 5 ("MSE vs reference EKF"; the reference has no EKF, SURVEY.md
+ * 8(f) f2), float64, one thread per sequence, all T steps in one launch:
+ *   predict  x- = f(x+, u_t) (the clamped vehicle_model.py:109-134 step), F = df/dx by central
+ *            differences (step 1e-6 max(1, |x_j|); clamped components give zero rows),
+ *            P- = F P+ F' + diag(Q)
+ *   update   H = rows 0,1,3,4,5; S = H P- H' + diag(R); K = P- H' S^-1 (Cholesky); x+ = x- + K (y_t - H x-);
+ *            P+ = (I - K H) P- (I - K H)' + K diag(R) K'   (Joseph form)
+ * y [B,5,T] measurements and u [B,2,T] controls in real units, x0 [B,6] initial estimate,
+ * P0 / Q [6] and R [5] diagonals; x_est [B,6,T] receives x+ after each step. */
+int traj_ekf_run_f64(const traj_vehicle_params* p, const traj_knet_limits* lim, double Ts, int B, int T,
+                     const double* y, const double* u, const double* x0, const double* P0, const double* Q,
+                     const double* R, double* x_est, void* stream);
 
 #ifdef __cplusplus
 }

@@ -110,3 +110,55 @@ def angular_mse_db(x_est_real, x_true_real, phi_idx=2):
     d = x_est_real - x_true_real
     d[:, phi_idx] = torch.atan2(torch.sin(d[:, phi_idx]), torch.cos(d[:, phi_idx]))
     return 10.0 * math.log10(float((d ** 2).mean()) + 1e-12)
+
+
+# ------------------------------------------------------------------ EKF baseline (no reference
+# counterpart: SURVEY.md 8(f) f2); the same algorithm as include/trajknet.h traj_ekf_run_f64, float64.
+def _veh_f64(x, d, de, p, Ts):
+    lo = [p["x_min"], p["y_min"], p["phi_min"], p["vx_min"], p["vy_min"], p["omega_min"]]
+    hi = [p["x_max"], p["y_max"], p["phi_max"], p["vx_max"], p["vy_max"], p["omega_max"]]
+    cl = lambda v, i: min(max(v, lo[i]), hi[i])   # noqa: E731
+    phi, vx, vy, om = cl(x[2], 2), cl(x[3], 3), cl(x[4], 4), cl(x[5], 5)
+    vx_eff = max(abs(vx), p["vx_zero"])
+    af = -math.atan2(om * p["lf"] + vy, vx_eff) + de
+    ar = math.atan2(om * p["lr"] - vy, vx_eff)
+    af = min(max(af, -p["maxAlpha"]), p["maxAlpha"])
+    Fyf = p["Df"] * math.sin(p["Cf"] * math.atan(p["Bf"] * af))
+    Fyr = p["Dr"] * math.sin(p["Cr"] * math.atan(p["Br"] * ar))
+    Frx = (p["Cm1"] - p["Cm2"] * vx_eff) * d - p["Cr0"] - p["Cr2"] * (vx_eff * vx_eff)
+    sp, cp, sd, cd = math.sin(phi), math.cos(phi), math.sin(de), math.cos(de)
+    xd = [vx * cp - vy * sp, vx * sp + vy * cp, om, (Frx - Fyf * sd + p["m"] * vy * om) / p["m"],
+          (Fyr + Fyf * cd - p["m"] * vx * om) / p["m"], (Fyf * p["lf"] * cd - Fyr * p["lr"]) / p["Iz"]]
+    return [cl(x[i] + Ts * xd[i], i) for i in range(6)]
+
+
+def ekf_run(p, Ts, y, u, x0, P0, Q, R):
+    """y [B,5,T], u [B,2,T], x0 [B,6] (numpy) -> [B,6,T]."""
+    import numpy as np
+    y, u, x0 = np.asarray(y, float), np.asarray(u, float), np.asarray(x0, float)
+    B, T = y.shape[0], y.shape[2]
+    H = np.zeros((5, 6))
+    for a, r in enumerate((0, 1, 3, 4, 5)):
+        H[a, r] = 1.0
+    out = np.zeros((B, 6, T))
+    for b in range(B):
+        x = x0[b].copy()
+        P = np.diag(P0)
+        for t in range(T):
+            d, de = u[b, 0, t], u[b, 1, t]
+            xm = np.array(_veh_f64(x, d, de, p, Ts))
+            F = np.zeros((6, 6))
+            for j in range(6):
+                h = 1e-6 * max(1.0, abs(x[j]))
+                xp, xq = x.copy(), x.copy()
+                xp[j] += h
+                xq[j] -= h
+                F[:, j] = (np.array(_veh_f64(xp, d, de, p, Ts)) - np.array(_veh_f64(xq, d, de, p, Ts))) / (2 * h)
+            Pm = F @ P @ F.T + np.diag(Q)
+            S = H @ Pm @ H.T + np.diag(R)
+            K = np.linalg.solve(S, H @ Pm).T
+            x = xm + K @ (y[b, :, t] - H @ xm)
+            A = np.eye(6) - K @ H
+            P = A @ Pm @ A.T + K @ np.diag(R) @ K.T
+            out[b, :, t] = x
+    return out

@@ -97,6 +97,8 @@ _SIGS = {
                                       _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_knet_gru_gates_f32": (C.c_int, [C.c_int, C.c_int, _V, _V, _V, _V, _V]),
     "traj_knet_update_f32": (C.c_int, [C.c_int, _V, _V, _V, _V, _V, _V]),
+    "traj_ekf_run_f64": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_double, C.c_int, C.c_int,
+                                   _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,
                                         _V, _V, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V, C.c_size_t, _V]),
 }

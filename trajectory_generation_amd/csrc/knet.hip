@@ -116,6 +116,138 @@ __global__ __launch_bounds__(256) void knet_update_kernel(int B, const float* __
     }
 }
 
+// ---------------------------------------------------------------- EKF baseline (float64)
+struct KPd {
+    double Cm1, Cm2, Cr0, Cr2, Br, Cr, Dr, Bf, Cf, Df, m, Iz, lf, lr, maxAlpha, vx_zero;
+    double lo[6], hi[6];
+};
+
+__device__ __forceinline__ double clampd_(double x, double lo, double hi) {
+    double t = (x < lo) ? lo : x;
+    return (t > hi) ? hi : t;
+}
+
+// vehicle_model.py:109-134 in float64: pre-clamped pt_f_cont, Euler step, clamp of all states
+__device__ void veh_f(const KPd& p, double Ts, const double* x, double d, double delta, double* xn) {
+    const double phi = clampd_(x[2], p.lo[2], p.hi[2]), vx = clampd_(x[3], p.lo[3], p.hi[3]);
+    const double vy = clampd_(x[4], p.lo[4], p.hi[4]), om = clampd_(x[5], p.lo[5], p.hi[5]);
+    const double avx = fabs(vx);
+    const double vx_eff = (avx > p.vx_zero) ? avx : p.vx_zero;
+    double af = -atan2(om * p.lf + vy, vx_eff) + delta;
+    const double ar = atan2(om * p.lr - vy, vx_eff);
+    af = clampd_(af, -p.maxAlpha, p.maxAlpha);
+    const double Fyf = p.Df * sin(p.Cf * atan(p.Bf * af));
+    const double Fyr = p.Dr * sin(p.Cr * atan(p.Br * ar));
+    const double Frx = (p.Cm1 - p.Cm2 * vx_eff) * d - p.Cr0 - p.Cr2 * (vx_eff * vx_eff);
+    double sphi, cphi, sd, cd;
+    sincos(phi, &sphi, &cphi);
+    sincos(delta, &sd, &cd);
+    const double xd[6] = {vx * cphi - vy * sphi, vx * sphi + vy * cphi, om,
+                          (Frx - Fyf * sd + p.m * vy * om) / p.m, (Fyr + Fyf * cd - p.m * vx * om) / p.m,
+                          (Fyf * p.lf * cd - Fyr * p.lr) / p.Iz};
+    for (int i = 0; i < 6; ++i) xn[i] = clampd_(x[i] + Ts * xd[i], p.lo[i], p.hi[i]);
+}
+
+__global__ __launch_bounds__(64) void ekf_kernel(KPd p, double Ts, int B, int T, const double* __restrict__ y,
+                                                 const double* __restrict__ u, const double* __restrict__ x0,
+                                                 const double* __restrict__ P0, const double* __restrict__ Q,
+                                                 const double* __restrict__ R, double* __restrict__ xo) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int hr[5] = {0, 1, 3, 4, 5};
+    double x[6], P[6][6];
+    for (int i = 0; i < 6; ++i) {
+        x[i] = x0[6 * b + i];
+        for (int j = 0; j < 6; ++j) P[i][j] = (i == j) ? P0[i] : 0.0;
+    }
+    for (int t = 0; t < T; ++t) {
+        const double d = u[((size_t)b * 2 + 0) * T + t], de = u[((size_t)b * 2 + 1) * T + t];
+        // predict
+        double xm[6], F[6][6];
+        veh_f(p, Ts, x, d, de, xm);
+        for (int j = 0; j < 6; ++j) {
+            const double h = 1e-6 * fmax(1.0, fabs(x[j]));
+            double xp[6], xq[6], fp[6], fq[6];
+            for (int i = 0; i < 6; ++i) {
+                xp[i] = x[i] + (i == j ? h : 0.0);
+                xq[i] = x[i] - (i == j ? h : 0.0);
+            }
+            veh_f(p, Ts, xp, d, de, fp);
+            veh_f(p, Ts, xq, d, de, fq);
+            for (int i = 0; i < 6; ++i) F[i][j] = (fp[i] - fq[i]) / (2.0 * h);
+        }
+        double FP[6][6], Pm[6][6];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < 6; ++k) s += F[i][k] * P[k][j];
+                FP[i][j] = s;
+            }
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < 6; ++k) s += FP[i][k] * F[j][k];
+                Pm[i][j] = s + (i == j ? Q[i] : 0.0);
+            }
+        // update: S = H Pm H' + R (5x5), Cholesky S = L L'
+        double S[5][5], L[5][5] = {};
+        for (int a = 0; a < 5; ++a)
+            for (int c = 0; c < 5; ++c) S[a][c] = Pm[hr[a]][hr[c]] + (a == c ? R[a] : 0.0);
+        for (int a = 0; a < 5; ++a) {
+            for (int c = 0; c <= a; ++c) {
+                double s = S[a][c];
+                for (int k = 0; k < c; ++k) s -= L[a][k] * L[c][k];
+                L[a][c] = (a == c) ? sqrt(s) : s / L[c][c];
+            }
+        }
+        // K' = S^-1 (H Pm) : solve L L' K' = H Pm (columns of K' per state)
+        double Kt[5][6];
+        for (int j = 0; j < 6; ++j) {
+            double z[5];
+            for (int a = 0; a < 5; ++a) {
+                double s = Pm[hr[a]][j];
+                for (int k = 0; k < a; ++k) s -= L[a][k] * z[k];
+                z[a] = s / L[a][a];
+            }
+            for (int a = 4; a >= 0; --a) {
+                double s = z[a];
+                for (int k = a + 1; k < 5; ++k) s -= L[k][a] * Kt[k][j];
+                Kt[a][j] = s / L[a][a];
+            }
+        }
+        double innov[5];
+        for (int a = 0; a < 5; ++a) innov[a] = y[((size_t)b * 5 + a) * T + t] - xm[hr[a]];
+        for (int i = 0; i < 6; ++i) {
+            double s = 0.0;
+            for (int a = 0; a < 5; ++a) s += Kt[a][i] * innov[a];
+            x[i] = xm[i] + s;
+        }
+        // Joseph form: P = A Pm A' + K R K', A = I - K H
+        double A[6][6];
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                double kh = 0.0;
+                for (int a = 0; a < 5; ++a) kh += (hr[a] == j) ? Kt[a][i] : 0.0;
+                A[i][j] = (i == j ? 1.0 : 0.0) - kh;
+            }
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < 6; ++k) s += A[i][k] * Pm[k][j];
+                FP[i][j] = s;
+            }
+        for (int i = 0; i < 6; ++i)
+            for (int j = 0; j < 6; ++j) {
+                double s = 0.0;
+                for (int k = 0; k < 6; ++k) s += FP[i][k] * A[j][k];
+                double kr = 0.0;
+                for (int a = 0; a < 5; ++a) kr += Kt[a][i] * R[a] * Kt[a][j];
+                P[i][j] = s + kr;
+            }
+        for (int i = 0; i < 6; ++i) xo[((size_t)b * 6 + i) * T + t] = x[i];
+    }
+}
+
 inline int nblk(long long n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -155,6 +287,21 @@ int traj_knet_update_f32(int B, const float* x_prior, const float* KG, const flo
     if (!x_prior || !KG || !dy || !innov_logit || !x_post) return TRAJ_E_ARG;
     hipLaunchKernelGGL(knet_update_kernel, dim3(nblk(B, 256)), dim3(256), 0, (hipStream_t)stream, B, x_prior, KG, dy,
                        innov_logit, x_post);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_ekf_run_f64(const traj_vehicle_params* p, const traj_knet_limits* lim, double Ts, int B, int T,
+                     const double* y, const double* u, const double* x0, const double* P0, const double* Q,
+                     const double* R, double* x_est, void* stream) {
+    if (!p || !lim || B < 0 || T < 0) return TRAJ_E_ARG;
+    if (B == 0 || T == 0) return TRAJ_OK;
+    if (!y || !u || !x0 || !P0 || !Q || !R || !x_est) return TRAJ_E_ARG;
+    KPd k{p->Cm1, p->Cm2, p->Cr0, p->Cr2, p->Br, p->Cr, p->Dr, p->Bf, p->Cf, p->Df, p->m, p->Iz, p->lf, p->lr,
+          p->maxAlpha, p->vx_zero,
+          {lim->x_min, lim->y_min, lim->phi_min, lim->vx_min, lim->vy_min, lim->omega_min},
+          {lim->x_max, lim->y_max, lim->phi_max, lim->vx_max, lim->vy_max, lim->omega_max}};
+    hipLaunchKernelGGL(ekf_kernel, dim3(nblk(B, 64)), dim3(64), 0, (hipStream_t)stream, k, Ts, B, T, y, u, x0, P0, Q,
+                       R, x_est);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 

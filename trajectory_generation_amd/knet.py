@@ -60,11 +60,11 @@ def knet_prior(params: dict, Ts: float, x_post, u, x_mean, x_std, y_mean, y_std,
     prior = torch.empty((B, 6), dtype=torch.float32, device=dev)
     m1y = torch.empty((B, 5), dtype=torch.float32, device=dev)
     dy = None if y is None else torch.empty((B, 5), dtype=torch.float32, device=dev)
-    flat = lambda t: None if t is None else t.reshape(-1).contiguous()   # noqa: E731
+    # bound to locals: a temporary's storage would go back to the allocator before the launch
+    norm = [None if t is None else t.reshape(-1).contiguous() for t in (x_mean, x_std, y_mean, y_std, u_mean, u_std)]
     _lib.check(_lib.lib().traj_knet_prior_f32(
         C.byref(params_struct(params)), C.byref(limits_struct(params)), float(Ts), B, _p(xp), _p(uu), _p(yy),
-        _p(flat(x_mean)), _p(flat(x_std)), _p(flat(y_mean)), _p(flat(y_std)), _p(flat(u_mean)), _p(flat(u_std)),
-        _p(prior), _p(m1y), _p(dy), _stream()), "traj_knet_prior_f32")
+        *[_p(t) for t in norm], _p(prior), _p(m1y), _p(dy), _stream()), "traj_knet_prior_f32")
     return prior, m1y, dy
 
 
@@ -237,8 +237,8 @@ class KalmanNetNN(nn.Module):
         KG = self.KGain_step(dy, self.m1x_prior.reshape(B, self.m))
         self.KGain = KG.reshape(self.batch_size, self.m, self.n)
         post = torch.empty((B, self.m), dtype=torch.float32, device=self.device)
-        _lib.check(_lib.lib().traj_knet_update_f32(B, _p(self.m1x_prior.reshape(B, self.m).contiguous()),
-                                                   _p(KG.contiguous()), _p(dy), _p(self.innov_logit.detach()),
+        prior, KGc = self.m1x_prior.reshape(B, self.m).contiguous(), KG.contiguous()
+        _lib.check(_lib.lib().traj_knet_update_f32(B, _p(prior), _p(KGc), _p(dy), _p(self.innov_logit.detach()),
                                                    _p(post), _stream()), "traj_knet_update_f32")
         self.m1x_posterior = post.unsqueeze(2)
         return self.m1x_posterior
@@ -316,3 +316,26 @@ class KNetSequenceRunner:
             self.graph.replay()
             out[:, :, t] = state["post"].squeeze(2)
         return out
+
+
+# --------------------------------------------------------------------------- EKF baseline (f2)
+# R: generation_type1.py:24-32 measurement noise (phi not measured); Q: process noise of the Euler
+# model, chosen for the synthetic data (the reference defines no EKF); P0: the initial-state spread.
+EKF_R = (0.05 ** 2, 0.05 ** 2, 0.010 ** 2, 0.003 ** 2, 0.030 ** 2)
+EKF_Q = (1e-6, 1e-6, 1e-5, 1e-4, 1e-4, 1e-2)
+EKF_P0 = (0.1, 0.1, 0.1, 0.1, 0.01, 0.1)
+
+
+def ekf_run(params: dict, Ts: float, y, u, x0, P0=EKF_P0, Q=EKF_Q, R=EKF_R):
+    """Batched EKF over the clamped vehicle model (include/trajknet.h traj_ekf_run_f64), float64.
+    y [B,5,T] real-unit measurements, u [B,2,T], x0 [B,6] -> estimates [B,6,T]."""
+    dev = require_gpu(y.device if torch.is_tensor(y) and y.is_cuda else None)
+    f64 = lambda a: torch.as_tensor(a, dtype=torch.float64, device=dev).contiguous()   # noqa: E731
+    yy, uu, xx = f64(y), f64(u), f64(x0).reshape(-1, 6)
+    B, T = yy.shape[0], yy.shape[2]
+    out = torch.empty((B, 6, T), dtype=torch.float64, device=dev)
+    p0, q, r = f64(P0), f64(Q), f64(R)     # kept alive until the launch is enqueued
+    _lib.check(_lib.lib().traj_ekf_run_f64(C.byref(params_struct(params)), C.byref(limits_struct(params)), float(Ts),
+                                           B, T, _p(yy), _p(uu), _p(xx), _p(p0), _p(q), _p(r), _p(out),
+                                           _stream()), "traj_ekf_run_f64")
+    return out
