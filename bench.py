@@ -1,9 +1,11 @@
 """bench.py -- MPC steps/sec on B parallel spline-tracking trajectories (BASELINE.json configs[1]).
 
 One bench step = one closed-loop step of MPC/main.py:85-101 for all B trajectories of this rank
-(reference window -> mpc_step -> Euler plant) = one traj_closed_loop_step call = two HIP launches
-(linearize_kernel: rollout + FD Jacobians; solve_kernel: window, condensing, ADMM + polish, plant).
-Inputs and state are resident in HBM for the whole timed region.
+(reference window -> mpc_step -> Euler plant) = one traj_closed_loop_step call = four HIP launches
+(rollout_kernel: nominal rollout; jac_kernel: FD Jacobians -> A, B, g; order_kernel: longest-first
+solve order; solve_kernel: window, condensing, ADMM + polish, plant, history).  Inputs and state are
+resident in HBM for the whole timed region.  The roofline object is solve_kernel's (the dominant
+kernel), timed with HIP events the library records on the launch stream around each kernel.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 20] [--dt 0.05]
   N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
@@ -18,6 +20,7 @@ baseline (the C oracle -- a restatement of the reference path -- on a bounded sa
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -29,6 +32,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+from trajectory_generation_amd import _lib  # noqa: E402
 from trajectory_generation_amd import batch as TB  # noqa: E402
 from trajectory_generation_amd.workload import make_workload  # noqa: E402
 
@@ -41,6 +45,11 @@ def algorithmic_bytes_per_traj(N: int, kmax: int) -> int:
     writes x 6, u_prev 2, hist_x 6, hist_u 2, status (4 B), iters (4 B)."""
     doubles = 6 + 2 + (N + 1) + 4 + kmax + 4 * (kmax - 1) + 6 + 2 + 6 + 2
     return 8 * doubles + 4 * 4
+
+
+def _capacity(n: int) -> int:
+    """solve_kernel instance the library launches for 2N QP variables (trajmpc.hip launch_mpc)."""
+    return next(c for c in (16, 32, 40, 64, 80) if n <= c)
 
 
 def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):
@@ -170,13 +179,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    L = _lib.lib()
+    _lib.check(L.traj_debug_kernel_timing(args.steps), "traj_debug_kernel_timing")
     t0 = time.perf_counter()
     for k in range(args.steps):
         t = args.warmup + k
-        ev[k][0].record()
         TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
-        ev[k][1].record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -187,7 +195,12 @@ def main():
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
 
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kms = (ctypes.c_double * 4)()
+    nts = ctypes.c_int(0)
+    _lib.check(L.traj_debug_kernel_times(kms, ctypes.byref(nts)), "traj_debug_kernel_times")
+    _lib.check(L.traj_debug_kernel_timing(0), "traj_debug_kernel_timing")
+    kernels_ms = dict(zip(("rollout_kernel", "jac_kernel", "order_kernel", "solve_kernel"), list(kms)))
+    kern_ms = kernels_ms["solve_kernel"]
     iters = it[args.warmup:].cpu().numpy().reshape(-1)
     stat = st[args.warmup:].cpu().numpy().reshape(-1)
     if rank != 0:
@@ -200,15 +213,16 @@ def main():
     kmax = int(paths.xk.shape[1])
     bytes_launch = B * algorithmic_bytes_per_traj(N, kmax)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = None
+    traffic = traffic_step = None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("batch") == B and tj.get("horizon") == N:
-                traffic = tj.get("hbm_bytes_per_launch")
+                traffic = tj.get("hbm_bytes_per_kernel", {}).get("solve_kernel")
+                traffic_step = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
-            traffic = None
+            traffic = traffic_step = None
     out = {
         "metric": "MPC steps/sec (batch=4096, N=20)" if (B == 4096 and N == 20) else f"MPC steps/sec (batch={B}, N={N})",
         "value": value,
@@ -227,8 +241,9 @@ def main():
                    "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "linearize_kernel<20,true> + solve_kernel<40,true> (one traj_closed_loop_step)",
-                     "kernel_ms": kern_ms, "bytes_per_launch": bytes_launch},
+                     "kernel": f"solve_kernel<{_capacity(2 * N)},true>", "kernel_ms": kern_ms,
+                     "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,
+                     "traffic_source": os.path.relpath(args.traffic_json, HERE) if traffic is not None else None},
         "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
                          "iters_max": int(iters.max()),
                          "status_hist": np.bincount(stat, minlength=7).tolist()},

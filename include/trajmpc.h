@@ -172,6 +172,13 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
  * NULL disables.  For profiling only; never enabled by the product path. */
 int traj_debug_set_stamps(long long* buf);
 
+/* Per-kernel timing of the next max_steps traj_closed_loop_step calls: HIP events recorded on the
+ * launch stream around rollout_kernel, jac_kernel, order_kernel and solve_kernel (0 frees them).
+ * traj_debug_kernel_times synchronizes, returns the mean milliseconds per step of the four kernels
+ * in ms[4] and the number of timed steps, and restarts the count.  For bench.py's roofline leg. */
+int traj_debug_kernel_timing(int max_steps);
+int traj_debug_kernel_times(double* ms, int* n_steps);
+
 #ifdef __cplusplus
 }
 #endif

@@ -14,10 +14,17 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = ("linearize_kernel", "solve_kernel")
+KERNELS = ("rollout_kernel", "jac_kernel", "order_kernel", "solve_kernel")
 
 
-def read_counter(d, name, batch):
+def expected_blocks(batch, horizon):
+    """Workgroups of each bench launch (trajmpc.hip traj_closed_loop_step)."""
+    return {"rollout_kernel": (batch + 63) // 64, "jac_kernel": (batch * horizon + 63) // 64, "order_kernel": 1,
+            "solve_kernel": batch}
+
+
+def read_counter(d, name, batch, horizon):
+    want = expected_blocks(batch, horizon)
     vals = defaultdict(list)
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
@@ -33,7 +40,7 @@ def read_counter(d, name, batch):
                     continue
                 grid = int(row.get("Grid_Size", "0") or 0)
                 wg = int(row.get("Workgroup_Size", "1") or 1)
-                if grid // max(wg, 1) != batch:
+                if grid // max(wg, 1) != want[k]:
                     continue
                 vals[(k, row.get("Dispatch_Id"))].append(float(row["Counter_Value"]))
     per_kernel = defaultdict(list)
@@ -50,8 +57,8 @@ def main():
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    fetch, nf = read_counter(a.fetch, "FETCH_SIZE", a.batch)
-    write, nw = read_counter(a.write, "WRITE_SIZE", a.batch)
+    fetch, nf = read_counter(a.fetch, "FETCH_SIZE", a.batch, a.horizon)
+    write, nw = read_counter(a.write, "WRITE_SIZE", a.batch, a.horizon)
     kib = 1024.0
     res = {"batch": a.batch, "horizon": a.horizon, "dispatches": {"fetch": nf, "write": nw},
            "raw_kib": {"FETCH_SIZE": fetch, "WRITE_SIZE": write},
@@ -60,8 +67,8 @@ def main():
     res["hbm_bytes_per_kernel"] = {k: res["fetch_bytes_per_launch"].get(k, 0.0) + res["write_bytes_per_launch"].get(k, 0.0)
                                    for k in KERNELS}
     res["hbm_bytes_per_launch"] = sum(res["hbm_bytes_per_kernel"].values())
-    res["note"] = ("per closed-loop step (linearize_kernel + solve_kernel launches); FETCH_SIZE x2 "
-                   "(gfx950 correction), KiB -> bytes")
+    res["note"] = ("hbm_bytes_per_launch = one closed-loop step (rollout + jac + order + solve launches); "
+                   "FETCH_SIZE x2 (gfx950 correction), KiB -> bytes")
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

@@ -7,6 +7,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 #include "../../include/trajmpc.h"
 #include "mpc_common.h"
@@ -209,6 +210,14 @@ static int check_cfg(const traj_mpc_config* c) {
 
 static long long* g_dbg = nullptr;  // diagnostics buffer (traj_debug_set_stamps)
 
+// per-kernel timing of traj_closed_loop_step (traj_debug_kernel_timing): 5 events per step bracket
+// rollout | jac | order | solve on the launch stream
+static std::vector<hipEvent_t> g_ev;
+static int g_ev_used = 0;
+static inline void stamp(int k, hipStream_t st) {
+    if ((size_t)(5 * g_ev_used + k) < g_ev.size()) hipEventRecord(g_ev[5 * g_ev_used + k], st);
+}
+
 static inline unsigned nblk(int B, int bs) { return (unsigned)((B + bs - 1) / bs); }
 
 }  // namespace tgmpc
@@ -221,6 +230,36 @@ int traj_abi_version(void) { return TRAJMPC_ABI_VERSION; }
 
 int traj_debug_set_stamps(long long* buf) {
     g_dbg = buf;
+    return TRAJ_OK;
+}
+
+int traj_debug_kernel_timing(int max_steps) {
+    for (hipEvent_t e : g_ev) hipEventDestroy(e);
+    g_ev.clear();
+    g_ev_used = 0;
+    if (max_steps < 0) return TRAJ_E_ARG;
+    g_ev.resize((size_t)5 * max_steps);
+    for (auto& e : g_ev)
+        if (hipEventCreate(&e) != hipSuccess) return TRAJ_E_LAUNCH;
+    return TRAJ_OK;
+}
+
+int traj_debug_kernel_times(double* ms, int* n_steps) {
+    if (!ms || !n_steps) return TRAJ_E_ARG;
+    for (int k = 0; k < 4; ++k) ms[k] = 0.0;
+    *n_steps = g_ev_used;
+    for (int s = 0; s < g_ev_used; ++s) {
+        hipEvent_t* e = &g_ev[5 * (size_t)s];
+        if (hipEventSynchronize(e[4]) != hipSuccess) return TRAJ_E_LAUNCH;
+        for (int k = 0; k < 4; ++k) {
+            float t = 0.f;
+            if (hipEventElapsedTime(&t, e[k], e[k + 1]) != hipSuccess) return TRAJ_E_LAUNCH;
+            ms[k] += t;
+        }
+    }
+    if (g_ev_used > 0)
+        for (int k = 0; k < 4; ++k) ms[k] /= g_ev_used;
+    g_ev_used = 0;
     return TRAJ_OK;
 }
 
@@ -414,14 +453,24 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.iters = iters;
     a.dbg = g_dbg;
     carve_workspace(a, workspace, B, c->N);
-    launch_linearize(a, (hipStream_t)stream, true);
+    hipStream_t st = (hipStream_t)stream;
+    const int nr = (B + 63) / 64, nj = (B * c->N + 63) / 64;
+    stamp(0, st);
+    hipLaunchKernelGGL(rollout_kernel<true>, dim3(nr), dim3(64), 0, st, a);
+    stamp(1, st);
+    hipLaunchKernelGGL(jac_kernel<true>, dim3(nj), dim3(256), 0, st, a);
+    stamp(2, st);
     if (t > 0) {
         // order this step's solves by the previous step's iteration counts (longest first)
         int* perm = (int*)(a.wsWarm + (size_t)B * 4);
-        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, (const double*)a.wsWarm, B, perm);
+        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, (const double*)a.wsWarm, B, perm);
         a.perm = perm;
     }
-    return launch_mpc(a, (hipStream_t)stream, 2);
+    stamp(3, st);
+    e = launch_mpc(a, st, 2);
+    stamp(4, st);
+    if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
+    return e;
 }
 
 }  // extern "C"
