@@ -10,7 +10,8 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtrajmpc.so")
+# TRAJMPC_LIB: an alternative build of the same library (kernel-variant experiments, tools/)
+LIB_PATH = os.environ.get("TRAJMPC_LIB") or os.path.join(_HERE, "libtrajmpc.so")
 CSRC = os.path.join(_HERE, "csrc")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "trajmpc.h")
 HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "trajknet.h")]

@@ -151,6 +151,28 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return r;
 }
 
+// Three-address fma (v_fma_f64 dst, a, b, c): keeps the compiler from turning a register-rotating
+// update into an in-place v_fmac plus register copies.
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Read NN (even) doubles from a 16-byte aligned LDS buffer as NN/2 ds_read_b128, all issued before
+// the first use (the default schedule waits on each read in turn under register pressure).
+template <int NN>
+__device__ __forceinline__ void lds_load_all(const double* p, double (&o)[NN]) {
+    const double2* p2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(p, 16));
+#pragma unroll
+    for (int i = 0; i < NN / 2; ++i) {
+        const double2 v = p2[i];
+        o[2 * i] = v.x;
+        o[2 * i + 1] = v.y;
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, NN / 2, 0);
+}
+
 // ---- DPP cross-lane moves (gfx9 data-parallel primitives: VALU, no LDS traffic) -------------
 // CTRL: 0x130 wave_shl:1 (lane t receives lane t+1), 0x138 wave_shr:1 (lane t-1), 0xB1 / 0x4E
 // quad_perm [1,0,3,2] / [2,3,0,1], 0x141 row_half_mirror, 0x140 row_mirror, 0x142 row_bcast:15,

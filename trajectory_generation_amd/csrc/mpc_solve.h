@@ -25,7 +25,7 @@ namespace tgmpc {
 // update, history).  A_k, B_k, g_k are read from a.Ad / a.Bd / a.gd ([B,N,36], [B,N,12], [B,N,6]).
 // =====================================================================================
 template <int NN, bool CLOSED>
-__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(2))) void solve_kernel(const KArgs a) {
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(NN <= 64 ? 2 : 1))) void solve_kernel(const KArgs a) {
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
@@ -380,7 +380,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
             double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
             double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
-            double* Dv = bcast(Dt);
+            double Dv[NN];
+            lds_load_all<NN>(bcast(Dt), Dv);   // all reads in flight at once (not one wait per read)
             cn = 0.0;
 #pragma unroll
             for (int j = 0; j < NN; ++j) {
@@ -453,7 +454,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         };
         double Krow[NN];
         auto Kmul = [&](double v) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
-            double* vb = bcast(v);
+            double vb[NN];
+            lds_load_all<NN>(bcast(v), vb);
             double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NN; ++j) sa[j & 7] = fma(Krow[j], vb[j], sa[j & 7]);
@@ -555,7 +557,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     v += (j == tt) ? (own ? dii : 1.0) : 0.0;    // identity padding for rows n..NN-1
                     v += (j == tt - 2) ? dm : 0.0;
                     v += (j == tt + 2) ? dp : 0.0;
-                    Krow[j] = v;
+                    // lanes >= NN hold exact zero rows (the receivers of the one-wave sweep below)
+                    Krow[j] = (WAVES == 1 && t >= NN) ? 0.0 : v;
                 }
             }
             // ---- sweep: Krow <- row t of K^{-1} (symmetric sweep operator, NN pivots) ----
@@ -566,6 +569,72 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             // (K symmetric: K[pv][c] = K[c][pv]).  Padding pivots (>= n) are identity and exact.
             bool ok = true;
             tic();
+            if constexpr (WAVES == 1 && NN <= 42) {
+                // One-wave sweep, ONE fma per entry and pivot.  The new pivot row (K_pj / d) is not
+                // formed in place (that needs a second operation on the pivot lane only) but in a
+                // RECEIVER lane holding an exact zero row: every lane computes
+                //     Krow[j] <- fma(be, pivot_row[j], Krow[j]),
+                // be = -K_tp / d on row lanes, 1 / d on the receiver (0 + pr/d, exact), and the old
+                // pivot lane's row is dropped.  Receivers are the spare lanes NN..63 (pivots < 64-NN),
+                // then the former pivot lanes 0.. (re-zeroed once), so row r ends in lane (r + NN) mod
+                // 64 and one ds_bpermute rotation puts it back in lane r.  The values are those of the
+                // two-operation form bit for bit (fma(be, pr, 1 * K) and fma(1/d, pr, 0 * K)).
+                // Rotated registers as below (pivot column in register 0); the update is written as
+                // three-address v_fma_f64 (fma3), so the rotation costs no register copies.
+                // Row lanes publish their column entry under the ROW they hold (rho), twice.
+                constexpr int SB = 2 * NN + 2;
+                constexpr int SPARE = 64 - NN;
+                int rho = t < NN ? t : -1;    // row held by this lane (-1: zero or dropped)
+                if (t < NN) {
+                    s_sw[t] = Krow[0];
+                    s_sw[t + NN] = Krow[0];
+                }
+#pragma nounroll
+                for (int pv = 0; pv < NN; ++pv) {
+                    if (NN > SPARE && pv == SPARE) {
+                        // lanes 0..SPARE-1 all pivoted (dropped rows): zero them, they receive next
+                        if (t < SPARE) {
+#pragma unroll
+                            for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
+                        }
+                    }
+                    __syncthreads();
+                    const int o = pv & 1;
+                    const double* prow = s_sw + o * SB + o + pv;
+                    const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
+                    double2 pr[NN / 2];
+#pragma unroll
+                    for (int i = 0; i < NN / 2; ++i) pr[i] = prow2[i];
+                    const double d = pr[0].x;
+                    ok = ok && (d > 0.0);
+                    const double dinv = rcp_nr(d);
+                    const int rl = pv < SPARE ? NN + pv : pv - SPARE;   // receiver lane (uniform)
+                    const bool recv = (t == rl);
+                    const double fd = Krow[0] * dinv;
+                    const double be = recv ? dinv : -fd;
+                    const double k0 = recv ? -dinv : fd;
+                    rho = recv ? pv : ((t == pv) ? -1 : rho);
+                    const double n0 = fma3(be, pr[0].y, Krow[1]);
+                    if (rho >= 0) {
+                        double* nb = s_sw + (o ^ 1) * SB + (o ^ 1);
+                        nb[rho] = n0;
+                        nb[rho + NN] = n0;
+                    }
+#pragma unroll
+                    for (int j = 2; j < NN; ++j) Krow[j - 1] = fma3(be, (j & 1) ? pr[j >> 1].y : pr[j >> 1].x, Krow[j]);
+                    Krow[0] = n0;
+                    Krow[NN - 1] = k0;
+                }
+                // row r sits in lane (r + NN) mod 64: rotate it back to lane r
+                const int src = ((t + NN) & 63) << 2;
+#pragma unroll
+                for (int j = 0; j < NN; ++j) {
+                    const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(Krow[j]));
+                    const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(Krow[j]));
+                    Krow[j] = __hiloint2double(hi, lo);
+                    __builtin_amdgcn_sched_barrier(0);   // one register at a time (no batch of 80 temporaries)
+                }
+            } else {
             {
                 // Pivot pv: K_tj <- K_tj - (K_tp / d) K_pj off the pivot row, K_pj / d on it, column
                 // pv <- K_tp / d (and -1/d on the pivot).  The next pivot's column (new Krow[0]) is
@@ -614,6 +683,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     Krow[0] = n0;
                     Krow[NN - 1] = k0;   // rotate: the pivot column moves to the end
                 }
+            }
             }
 #pragma unroll
             for (int j = 0; j < NN; ++j) Krow[j] = -Krow[j];
