@@ -173,7 +173,23 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     stamp(2, __builtin_amdgcn_s_memrealtime());   // 100 MHz wall clock (comparable across XCDs)
     // ---- 3. condensed QP (:180-250) --------------------------------------------------
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
-    {
+    if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
+        // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
+        // at once (one L2/MALL latency, no VGPRs); the three blocks are contiguous in s_big as double2
+        // [A 18N | B 6N | g 3N].  Chunk r lands at s_big2[r NT + lane]; lanes past the end re-load
+        // the last element into the unused tail of s_big (NBIG >= 2 NT ceil(27 NM / NT)).
+        constexpr int MAXV = (27 * NM + NT - 1) / NT;
+        static_assert(NBIG >= 2 * NT * MAXV, "s_big too small for the LDS-DMA staging tail");
+        const int nA = 18 * N, nB = 6 * N, nT = 27 * N;
+#pragma unroll
+        for (int r = 0; r < MAXV; ++r) {
+            const int i = min(t + r * NT, nT - 1);
+            const double2* src = (i < nA) ? reinterpret_cast<const double2*>(gA) + i
+                               : (i < nA + nB) ? reinterpret_cast<const double2*>(gB) + (i - nA)
+                                               : reinterpret_cast<const double2*>(gg) + (i - nA - nB);
+            __builtin_amdgcn_global_load_lds(src, reinterpret_cast<double2*>(s_big) + r * NT + wid * 64, 16, 0, 0);
+        }
+    } else {
         for (int i = t; i < 36 * N; i += NT) s_big[i] = gA[i];
         for (int i = t; i < 12 * N; i += NT) s_big[36 * N + i] = gB[i];
         for (int i = t; i < 6 * N; i += NT) s_big[48 * N + i] = gg[i];
