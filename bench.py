@@ -143,6 +143,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-knet", action="store_true", help="skip the KalmanNet measurement (configs[4])")
+    ap.add_argument("--per-step", action="store_true",
+                    help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
     args = ap.parse_args()
@@ -172,8 +174,13 @@ def main():
     st = torch.empty((T, B), dtype=torch.int32, device=dev)
     it = torch.empty((T, B), dtype=torch.int32, device=dev)
 
-    for t in range(args.warmup):
-        TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
+    fused = not args.per_step
+    if fused:
+        if args.warmup:
+            TB.closed_loop_run(x, u, paths, vref, cfg, None, 0, args.warmup, hx, hu, st[:args.warmup], it[:args.warmup])
+    else:
+        for t in range(args.warmup):
+            TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -182,9 +189,13 @@ def main():
     L = _lib.lib()
     _lib.check(L.traj_debug_kernel_timing(args.steps), "traj_debug_kernel_timing")
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        t = args.warmup + k
-        TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
+    if fused:   # all K steps in one launch (traj_closed_loop_run: bit-identical to K step launches)
+        w0 = args.warmup
+        TB.closed_loop_run(x, u, paths, vref, cfg, None, w0, args.steps, hx, hu, st[w0:], it[w0:])
+    else:
+        for k in range(args.steps):
+            t = args.warmup + k
+            TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -200,7 +211,10 @@ def main():
     _lib.check(L.traj_debug_kernel_times(kms, ctypes.byref(nts)), "traj_debug_kernel_times")
     _lib.check(L.traj_debug_kernel_timing(0), "traj_debug_kernel_timing")
     kernels_ms = dict(zip(("rollout_kernel", "jac_kernel", "order_kernel", "solve_kernel"), list(kms)))
+    if fused:   # one launch = args.steps closed-loop steps, linearization inside the solve kernel
+        kernels_ms = {"solve_kernel": kernels_ms["solve_kernel"]}
     kern_ms = kernels_ms["solve_kernel"]
+    steps_per_launch = args.steps if fused else 1
     iters = it[args.warmup:].cpu().numpy().reshape(-1)
     stat = st[args.warmup:].cpu().numpy().reshape(-1)
     if rank != 0:
@@ -211,7 +225,7 @@ def main():
     total = world * B * args.steps
     value = total / elapsed
     kmax = int(paths.xk.shape[1])
-    bytes_launch = B * algorithmic_bytes_per_traj(N, kmax)
+    bytes_launch = B * algorithmic_bytes_per_traj(N, kmax) * steps_per_launch
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = traffic_step = None
     if os.path.exists(args.traffic_json):
@@ -219,8 +233,9 @@ def main():
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("batch") == B and tj.get("horizon") == N:
-                traffic = tj.get("hbm_bytes_per_kernel", {}).get("solve_kernel")
-                traffic_step = tj.get("hbm_bytes_per_launch")
+                if bool(tj.get("fused", False)) == fused and int(tj.get("steps_per_launch", 1)) == steps_per_launch:
+                    traffic = tj.get("hbm_bytes_per_kernel", {}).get("solve_kernel")
+                    traffic_step = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = traffic_step = None
     out = {
@@ -238,10 +253,13 @@ def main():
         "data": "synthetic",
         "config": {"workload": f"closed-loop {args.kind}-tracking MPC, {B} trajectories/GPU, N={N}, dt={Ts}s",
                    "global_batch": world * B, "horizon": N, "dt": Ts, "parallelism": f"shard{world}",
-                   "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64"},
+                   "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64",
+                   "launch": "fused traj_closed_loop_run" if fused else "traj_closed_loop_step per step"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": f"solve_kernel<{_capacity(2 * N)},true>", "kernel_ms": kern_ms,
+                     "kernel": f"solve_kernel<{_capacity(2 * N)},true>" + (
+                         f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
+                     "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
                      "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,
                      "traffic_source": os.path.relpath(args.traffic_json, HERE) if traffic is not None else None},
         "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),

@@ -164,11 +164,23 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
                           double* hist_u, int* status, int* iters, void* workspace, size_t workspace_bytes,
                           void* stream);
 
+/* The same closed loop for `steps` consecutive steps t0 .. t0+steps-1 in ONE launch (the fused
+ * form): every instance runs its own steps back to back in one workgroup, with the linearization
+ * (rollout + Jacobians) inside the workgroup and the state, u_prev and warm-start rho kept on chip,
+ * so no instance waits for the slowest instance of a step.  Results are bit-identical to `steps`
+ * calls of traj_closed_loop_step.  status / iters (optional) are [steps, B]; hist_x / hist_u as
+ * above with t0 + steps <= hist_T; x / u_prev hold the final state. */
+int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
+                         double* x, double* u_prev, const double* vref, int t0, int steps, int hist_T,
+                         double* hist_x, double* hist_u, int* status, int* iters, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
 /* ---- diagnostics ----
- * Subsequent MPC launches write, per instance b, 16 int64 slots at buf[16 b ..] (device memory):
+ * Subsequent MPC launches write, per instance b, 32 int64 slots at buf[32 b ..] (device memory):
  * [0..7] s_memtime at phase boundaries (start, inputs, rollout, linearization, condensing,
  * scaling, solver end, outputs), [8] KKT factorizations, [9] ADMM iterations, [10] polish passes,
- * [11] cycles in residual checks, [12] cycles in factorizations, [13] cycles in polish, [14] checks.
+ * [11] cycles in residual checks, [12] cycles in factorizations, [13] cycles in polish, [14] checks,
+ * [16..19] s_memtime inside the condensing phase (staging issued, staging landed, stage loop, P rows).
  * NULL disables.  For profiling only; never enabled by the product path. */
 int traj_debug_set_stamps(long long* buf);
 

@@ -332,6 +332,34 @@ def test_closed_loop_history_matches_single_steps(gpu):
         assert np.array_equal(res["X"].cpu().numpy()[:, t + 1], x)
 
 
+@pytest.mark.parametrize("N,warm,mode", [(20, 1, 0), (20, 0, 0), (8, 1, 0), (40, 1, 0), (20, 1, 1)])
+def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
+    """traj_closed_loop_run (one launch, in-workgroup linearization, on-chip state) equals the per-step
+    launches bit for bit: histories, statuses, iteration counts; also when split into two runs."""
+    from trajectory_generation_amd.workload import make_workload
+    Ts, T, B = 0.05, 24, 96
+    w = make_workload(B, N, Ts, kind="mixed" if N == 40 else "spline", seed=6)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=warm, polish_mode=mode)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    fus = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    for k in ("X", "U", "status", "iters"):
+        assert torch.equal(per[k], fus[k]), k
+    # two fused launches (t0 = 0 and t0 = 10) continue exactly (warm record carried in the workspace)
+    x = torch.as_tensor(w["x0"], device=gpu).clone()
+    u = torch.as_tensor(w["u0"], device=gpu).clone()
+    vr = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=gpu)
+    hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=gpu)
+    hu = torch.empty((B, T, 2), dtype=torch.float64, device=gpu)
+    hx[:, 0] = x
+    st = torch.empty((T, B), dtype=torch.int32, device=gpu)
+    it = torch.empty((T, B), dtype=torch.int32, device=gpu)
+    TB.closed_loop_run(x, u, paths, vr, cfg, None, 0, 10, hx, hu, st[:10], it[:10])
+    TB.closed_loop_run(x, u, paths, vr, cfg, None, 10, T - 10, hx, hu, st[10:], it[10:])
+    assert torch.equal(hx, per["X"]) and torch.equal(hu, per["U"])
+    assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"])
+
+
 # ------------------------------------------------------------------ drop-in module
 
 def test_dropin_mpc_step_contract(gpu, oracle_lib):

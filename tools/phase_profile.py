@@ -5,7 +5,7 @@ import numpy as np, torch
 from trajectory_generation_amd import batch as TB, _lib
 from trajectory_generation_amd.workload import make_workload
 
-def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
+def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
     dev = TB.require_gpu()
     w = make_workload(B, N, Ts, kind=kind)
     paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
@@ -14,10 +14,15 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
     for t in range(warm):
         TB.closed_loop_step(x, u, paths, vref, cfg, None, t)
-    dbg = torch.zeros((B, 16), dtype=torch.int64, device=dev)
+    dbg = torch.zeros((B, 32), dtype=torch.int64, device=dev)
     _lib.lib().traj_debug_set_stamps(C.c_void_p(dbg.data_ptr()))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(); TB.closed_loop_step(x, u, paths, vref, cfg, None, warm); e1.record()
+    e0.record()
+    if fused:   # one fused launch of `fused` steps; the stamps hold each instance's last step
+        TB.closed_loop_run(x, u, paths, vref, cfg, None, warm, fused)
+    else:
+        TB.closed_loop_step(x, u, paths, vref, cfg, None, warm)
+    e1.record()
     torch.cuda.synchronize()
     _lib.lib().traj_debug_set_stamps(None)
     d = dbg.cpu().numpy()
@@ -28,6 +33,9 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     print("phase       median      p90       max   (cycles)")
     for i, nm in enumerate(names):
         print(f"{nm:10s} {np.median(ph[:, i]):9.0f} {np.percentile(ph[:, i], 90):9.0f} {ph[:, i].max():9.0f}")
+    sub = np.diff(d[:, [1, 16, 17, 18, 19, 4]], axis=1)
+    for i, nm in enumerate(["  window/stage-issue", "  sincos+landed", "  stage loop", "  P rows", "  penalties"]):
+        print(f"{nm:22s} {np.median(sub[:, i]):9.0f} {np.percentile(sub[:, i], 90):9.0f}")
     tot = d[:, 7] - d[:, 0]
     print(f"{'total':10s} {np.median(tot):9.0f} {np.percentile(tot, 90):9.0f} {tot.max():9.0f}")
     it, nf, ps = d[:, 9], d[:, 8], d[:, 10]
@@ -53,4 +61,5 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0):
     print("in-kernel clock (median over instances): %.2f GHz" % np.median(clk))
 
 if __name__ == "__main__":
-    main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0, warm=int(sys.argv[2]) if len(sys.argv) > 2 else 5)
+    main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0, warm=int(sys.argv[2]) if len(sys.argv) > 2 else 5,
+         fused=int(sys.argv[3]) if len(sys.argv) > 3 else 0)

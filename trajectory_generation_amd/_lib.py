@@ -104,6 +104,8 @@ _SIGS = {
                                    _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,
                                         _V, _V, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V, C.c_size_t, _V]),
+    "traj_closed_loop_run": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,
+                                        _V, _V, _V, C.c_int, C.c_int, C.c_int, _V, _V, _V, _V, _V, C.c_size_t, _V]),
 }
 
 _lib = None

@@ -311,8 +311,23 @@ def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=Non
         _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()), "traj_closed_loop_step")
 
 
-def run_closed_loop(x0, u0, paths: PathSet, vref, T, cfg: MpcConfig, params=None, record=True) -> dict:
-    """T closed-loop steps (MPC/main.py:85-101) for B trajectories, all on the device.
+def closed_loop_run(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None, t0=0, steps=1, hist_x=None,
+                    hist_u=None, status=None, iters=None):
+    """Steps t0 .. t0+steps-1 of MPC/main.py:85-101 in ONE fused launch (traj_closed_loop_run), bit-identical
+    to `steps` closed_loop_step calls; x, u_prev updated in place; status / iters [steps, B]."""
+    B = x.shape[0]
+    ps = paths.struct()
+    T = hist_u.shape[1] if hist_u is not None else 0
+    ws = workspace(B, cfg.N, x.device)
+    _lib.check(_lib.lib().traj_closed_loop_run(
+        C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t0),
+        int(steps), int(T), _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()),
+        "traj_closed_loop_run")
+
+
+def run_closed_loop(x0, u0, paths: PathSet, vref, T, cfg: MpcConfig, params=None, record=True, fused=True) -> dict:
+    """T closed-loop steps (MPC/main.py:85-101) for B trajectories, all on the device: one fused launch
+    (closed_loop_run), or one launch sequence per step (fused=False; identical results).
 
     Returns X [B,T+1,6] (X[:,0] = x0), U [B,T,2], status [T,B], iters [T,B] (torch.cuda)."""
     x = _dev(x0, (-1, 6)).clone()
@@ -328,6 +343,9 @@ def run_closed_loop(x0, u0, paths: PathSet, vref, T, cfg: MpcConfig, params=None
         hx[:, 0] = x
     st = torch.empty((T, B), dtype=torch.int32, device=dev)
     it = torch.empty((T, B), dtype=torch.int32, device=dev)
-    for t in range(T):
-        closed_loop_step(x, u, paths, vr, cfg, params, t, hx, hu, st[t], it[t])
+    if fused:
+        closed_loop_run(x, u, paths, vr, cfg, params, 0, T, hx, hu, st, it)
+    else:
+        for t in range(T):
+            closed_loop_step(x, u, paths, vr, cfg, params, t, hx, hu, st[t], it[t])
     return dict(X=hx, U=hu, status=st, iters=it, x=x, u=u)

@@ -72,6 +72,7 @@ struct KArgs {
     double* wsXF;            // rollout record (x_k, f_k) per stage: [B,N,12]
     double* wsWarm;          // closed loop: per instance [rho, valid, ADMM iterations, 0] of the previous step
     const int* perm;         // closed loop: instance order (longest previous solve first), or null
+    int nsteps;              // > 0: fused closed loop, nsteps steps per launch (status / iters [nsteps, B])
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

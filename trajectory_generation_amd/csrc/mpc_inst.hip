@@ -12,11 +12,12 @@
 namespace tgmpc {
 
 // mode 0: MPC step, 1: QP only (A/B/g given), 2: closed-loop step (the linearization launches are
-// issued by the caller, trajmpc.hip)
+// issued by the caller, trajmpc.hip), 3: fused closed loop of a.nsteps steps (linearization inside)
 int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
     constexpr int NN = TGMPC_NN;
     dim3 grid(a.B), sblock(((NN + 63) / 64) * 64);
-    if (mode == 2) hipLaunchKernelGGL((solve_kernel<NN, true>), grid, sblock, 0, st, a);
+    if (mode == 3) hipLaunchKernelGGL((solve_kernel<NN, true, true>), grid, sblock, 0, st, a);
+    else if (mode == 2) hipLaunchKernelGGL((solve_kernel<NN, true>), grid, sblock, 0, st, a);
     else hipLaunchKernelGGL((solve_kernel<NN, false>), grid, sblock, 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -22,6 +22,30 @@
 
 namespace tgmpc {
 
+// f of the nominal rollout (mpc_6stati.py:55-71 with the tire model of :25-53), in the form the fused
+// kernel evaluates lane-parallel (block_linearize): the Pacejka sine taken from sincos, like sin/cos(phi).
+__device__ __forceinline__ void rollout_f(const VP& p, const double* x, double d, double delta, double sd, double cd,
+                                          double* xd) {
+    const double phi = x[2], vx = x[3], vy = x[4], omega = x[5];
+    const double avx = fabs(vx);
+    const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
+    const double vx_eff = np_sign(vx) * mx;
+    const double alpha_f = clampd(-atan2(omega * p.lf + vy, vx_eff) + delta, -p.maxAlpha, p.maxAlpha);
+    const double alpha_r = clampd(atan2(omega * p.lr - vy, vx_eff), -p.maxAlpha, p.maxAlpha);
+    double sf, cf, sr, cr, sphi, cphi;
+    sincos(p.Cf * atan(p.Bf * alpha_f), &sf, &cf);
+    sincos(p.Cr * atan(p.Br * alpha_r), &sr, &cr);
+    sincos(phi, &sphi, &cphi);
+    const double Fy_f = p.Df * sf, Fy_r = p.Dr * sr;
+    const double Frx = (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
+    xd[0] = vx * cphi - vy * sphi;
+    xd[1] = vx * sphi + vy * cphi;
+    xd[2] = omega;
+    xd[3] = (1.0 / p.m) * (Frx - Fy_f * sd + p.m * vy * omega);
+    xd[4] = (1.0 / p.m) * (Fy_r + Fy_f * cd - p.m * vx * omega);
+    xd[5] = (1.0 / p.Iz) * (Fy_f * p.lf * cd - Fy_r * p.lr);
+}
+
 template <bool CLOSED>
 __global__ __launch_bounds__(64) void rollout_kernel(const KArgs a) {
     const int b = blockIdx.x * 64 + threadIdx.x;
@@ -38,7 +62,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KArgs a) {
     sincos(u1, &sd, &cd);
     double* rec = a.wsXF + (size_t)b * N * 12;
     for (int k = 0; k < N; ++k) {
-        f_cont_sc(p, x, u0, u1, sd, cd, f);
+        rollout_f(p, x, u0, u1, sd, cd, f);
         for (int i = 0; i < 6; ++i) {
             rec[12 * k + i] = x[i];
             rec[12 * k + 6 + i] = f[i];
@@ -89,6 +113,88 @@ __device__ __forceinline__ void f_full(const VP& p, double vx, double vy, double
             long_force(p, vx, d), xd);
 }
 
+// Jacobian column of state `grp` (0 vx, 1 vy, 2 omega) at rollout point xb with input (d, de), by
+// central differences on full f evaluations (one code path for the three columns: the perturbed
+// component is selected, the others are the reference's x_i + 0.0).
+__device__ __forceinline__ void state_column(const VP& p, const double* xb, double d, double de, int grp, double* J) {
+    const double eps = 1e-5;
+    const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
+    double sphi, cphi, sd, cd;
+    sincos(phi, &sphi, &cphi);
+    sincos(de, &sd, &cd);
+    double fp[6], fm[6];
+    f_full(p, grp == 0 ? xb[3] + eps : vx, grp == 1 ? xb[4] + eps : vy, grp == 2 ? xb[5] + eps : om, sphi, cphi, d,
+           de, sd, cd, fp);
+    f_full(p, grp == 0 ? xb[3] - eps : vx, grp == 1 ? xb[4] - eps : vy, grp == 2 ? xb[5] - eps : om, sphi, cphi, d,
+           de, sd, cd, fm);
+    for (int r = 0; r < 6; ++r) J[r] = (fp[r] - fm[r]) / (2.0 * eps);
+}
+
+// The phi, d and delta columns (Jphi, Jd, Jde), which reuse the base tire evaluation.
+__device__ __forceinline__ void cheap_columns(const VP& p, const double* xb, double d, double de, double* Jphi,
+                                              double* Jd, double* Jde) {
+    const double eps = 1e-5;
+    const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
+    double sphi, cphi, sd, cd;
+    sincos(phi, &sphi, &cphi);
+    sincos(de, &sd, &cd);
+    double fp[6], fm[6];
+    const Tire t0 = tire_angles(p, vx, vy, om);
+    const double Ff0 = front_force(p, t0.atf, de), Fr0 = rear_force(p, t0.atr), Fx0 = long_force(p, vx, d);
+    {   // phi: only sin/cos(phi) change
+        double sp, cp, sm, cm;
+        sincos(xb[2] + eps, &sp, &cp);
+        sincos(xb[2] - eps, &sm, &cm);
+        f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
+        f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
+        for (int r = 0; r < 6; ++r) Jphi[r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    {   // d: only the longitudinal force changes
+        f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d + eps), fp);
+        f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d - eps), fm);
+        for (int r = 0; r < 6; ++r) Jd[r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    {   // delta: front force and sin/cos(delta) change
+        double sp, cp, sm, cm;
+        sincos(de + eps, &sp, &cp);
+        sincos(de - eps, &sm, &cm);
+        f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
+        f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
+        for (int r = 0; r < 6; ++r) Jde[r] = (fp[r] - fm[r]) / (2.0 * eps);
+    }
+    // a -0.0 among the components the input columns pass through: evaluate those two columns on
+    // the reference's exact vectors, f(x, u +- du) with u_other + 0.0 (signed zeros match too)
+    if ((__builtin_signbit(xb[2]) && xb[2] == 0.0) || (__builtin_signbit(xb[3]) && xb[3] == 0.0) ||
+        (__builtin_signbit(xb[4]) && xb[4] == 0.0) || (__builtin_signbit(xb[5]) && xb[5] == 0.0) ||
+        (__builtin_signbit(d) && d == 0.0) || (__builtin_signbit(de) && de == 0.0)) {
+        for (int cu = 0; cu < 2; ++cu) {
+            const double up[2] = {cu == 0 ? d + eps : d + 0.0, cu == 1 ? de + eps : de + 0.0};
+            const double um[2] = {cu == 0 ? d - eps : d + 0.0, cu == 1 ? de - eps : de + 0.0};
+            double xc[6];
+            for (int i = 0; i < 6; ++i) xc[i] = xb[i];
+            f_cont(p, xc, up, fp);
+            f_cont(p, xc, um, fm);
+            for (int r = 0; r < 6; ++r) (cu == 0 ? Jd : Jde)[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        }
+    }
+}
+
+// :106-108 for one stage: A = I + Ts Jx, B = Ts Ju (columns X, Y of Jx exactly zero)
+__device__ __forceinline__ double a_entry(int r, int cc, double Ts, double Jrc) {
+    return ((r == cc) ? 1.0 : 0.0) + Ts * Jrc;
+}
+// g = x + Ts f - A x - B u  (f = the rollout's f(x_k, u))
+__device__ __forceinline__ void g_stage(const double* A, const double* Bm, const double* xb, const double* fk, double d,
+                                       double de, double Ts, double* g) {
+    for (int r = 0; r < 6; ++r) {
+        double ax = 0.0, bu = 0.0;
+        for (int cc = 0; cc < 6; ++cc) ax += A[6 * r + cc] * xb[cc];
+        bu += Bm[2 * r] * d;
+        bu += Bm[2 * r + 1] * de;
+        g[r] = xb[r] + Ts * fk[r] - ax - bu;
+    }
+}
+
 // One workgroup = 4 waves x 64 stages: waves 0-2 form the vx / vy / omega columns of their 64
 // stages (a full tire evaluation per side), wave 3 the base tire and the cheap phi / d / delta
 // columns, then assembles A_k, B_k, g_k from the columns staged in LDS (wave-uniform branches).
@@ -102,93 +208,116 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
     const int b = valid ? gs / N : 0, k = valid ? gs - b * N : 0;
     const traj_vehicle_params& p = a.p;
     const double Ts = a.c.Ts;
-    const double eps = 1e-5;
     const double* rec = a.wsXF + ((size_t)b * N + k) * 12;
     const double* us = CLOSED ? a.u_state + 2 * (size_t)b : a.u_prev + 2 * (size_t)b;
     double xb[6];
     for (int i = 0; i < 6; ++i) xb[i] = valid ? rec[i] : 0.0;
     const double d = valid ? us[0] : 0.0, de = valid ? us[1] : 0.0;
-    // unperturbed components as the reference's x + dx carries them (x_i + 0.0)
-    const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
-    double sphi, cphi, sd, cd;
-    sincos(phi, &sphi, &cphi);
-    sincos(de, &sd, &cd);
-    double fp[6], fm[6];
     double (*J)[6] = sJ[s];
-    if (grp == 0) {            // vx
-        f_full(p, xb[3] + eps, vy, om, sphi, cphi, d, de, sd, cd, fp);
-        f_full(p, xb[3] - eps, vy, om, sphi, cphi, d, de, sd, cd, fm);
-        for (int r = 0; r < 6; ++r) J[1][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    } else if (grp == 1) {     // vy
-        f_full(p, vx, xb[4] + eps, om, sphi, cphi, d, de, sd, cd, fp);
-        f_full(p, vx, xb[4] - eps, om, sphi, cphi, d, de, sd, cd, fm);
-        for (int r = 0; r < 6; ++r) J[2][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    } else if (grp == 2) {     // omega
-        f_full(p, vx, vy, xb[5] + eps, sphi, cphi, d, de, sd, cd, fp);
-        f_full(p, vx, vy, xb[5] - eps, sphi, cphi, d, de, sd, cd, fm);
-        for (int r = 0; r < 6; ++r) J[3][r] = (fp[r] - fm[r]) / (2.0 * eps);
-    } else {                   // base tire; phi, d, delta
-        const Tire t0 = tire_angles(p, vx, vy, om);
-        const double Ff0 = front_force(p, t0.atf, de), Fr0 = rear_force(p, t0.atr), Fx0 = long_force(p, vx, d);
-        {   // phi: only sin/cos(phi) change
-            double sp, cp, sm, cm;
-            sincos(xb[2] + eps, &sp, &cp);
-            sincos(xb[2] - eps, &sm, &cm);
-            f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
-            f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
-            for (int r = 0; r < 6; ++r) J[0][r] = (fp[r] - fm[r]) / (2.0 * eps);
-        }
-        {   // d: only the longitudinal force changes
-            f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d + eps), fp);
-            f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d - eps), fm);
-            for (int r = 0; r < 6; ++r) J[4][r] = (fp[r] - fm[r]) / (2.0 * eps);
-        }
-        {   // delta: front force and sin/cos(delta) change
-            double sp, cp, sm, cm;
-            sincos(de + eps, &sp, &cp);
-            sincos(de - eps, &sm, &cm);
-            f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
-            f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
-            for (int r = 0; r < 6; ++r) J[5][r] = (fp[r] - fm[r]) / (2.0 * eps);
-        }
-        // a -0.0 among the components the input columns pass through: evaluate those two columns on
-        // the reference's exact vectors, f(x, u +- du) with u_other + 0.0 (signed zeros match too)
-        if ((__builtin_signbit(xb[2]) && xb[2] == 0.0) || (__builtin_signbit(xb[3]) && xb[3] == 0.0) ||
-            (__builtin_signbit(xb[4]) && xb[4] == 0.0) || (__builtin_signbit(xb[5]) && xb[5] == 0.0) ||
-            (__builtin_signbit(d) && d == 0.0) || (__builtin_signbit(de) && de == 0.0)) {
-            for (int cu = 0; cu < 2; ++cu) {
-                const double up[2] = {cu == 0 ? d + eps : d + 0.0, cu == 1 ? de + eps : de + 0.0};
-                const double um[2] = {cu == 0 ? d - eps : d + 0.0, cu == 1 ? de - eps : de + 0.0};
-                f_cont(p, xb, up, fp);
-                f_cont(p, xb, um, fm);
-                for (int r = 0; r < 6; ++r) J[4 + cu][r] = (fp[r] - fm[r]) / (2.0 * eps);
-            }
-        }
-    }
+    if (grp < 3) state_column(p, xb, d, de, grp, J[1 + grp]);   // vx, vy, omega
+    else cheap_columns(p, xb, d, de, J[0], J[4], J[5]);        // phi, d, delta
     __syncthreads();
     if (grp != 3 || !valid) return;
     // :106-108  A = I + Ts Jx ; B = Ts Ju ; g = x + Ts f - A x - B u   (f = the rollout's f(x_k, u))
-    double A[36], Bm[12];
+    double A[36], Bm[12], g[6];
     for (int r = 0; r < 6; ++r) {
-        A[6 * r + 0] = (r == 0 ? 1.0 : 0.0) + Ts * 0.0;
-        A[6 * r + 1] = (r == 1 ? 1.0 : 0.0) + Ts * 0.0;
-        for (int cc = 2; cc < 6; ++cc) A[6 * r + cc] = ((r == cc) ? 1.0 : 0.0) + Ts * J[cc - 2][r];
+        A[6 * r + 0] = a_entry(r, 0, Ts, 0.0);
+        A[6 * r + 1] = a_entry(r, 1, Ts, 0.0);
+        for (int cc = 2; cc < 6; ++cc) A[6 * r + cc] = a_entry(r, cc, Ts, J[cc - 2][r]);
         Bm[2 * r + 0] = Ts * J[4][r];
         Bm[2 * r + 1] = Ts * J[5][r];
     }
+    g_stage(A, Bm, xb, rec + 6, d, de, Ts, g);
     const size_t o = (size_t)b * N + k;
     double* wA = a.wsA + o * 36;
     double* wB = a.wsB + o * 12;
     double* wg = a.wsg + o * 6;
     for (int i = 0; i < 36; ++i) wA[i] = A[i];
     for (int i = 0; i < 12; ++i) wB[i] = Bm[i];
-    for (int r = 0; r < 6; ++r) {
-        double ax = 0.0, bu = 0.0;
-        for (int cc = 0; cc < 6; ++cc) ax += A[6 * r + cc] * xb[cc];
-        bu += Bm[2 * r] * d;
-        bu += Bm[2 * r + 1] * de;
-        wg[r] = xb[r] + Ts * rec[6 + r] - ax - bu;
+    for (int r = 0; r < 6; ++r) wg[r] = g[r];
+}
+
+// In-workgroup linearization for the fused closed loop (traj_closed_loop_run): rollout_kernel's
+// and jac_kernel's arithmetic (the same device functions) for ONE instance and NT threads, with
+// A_k, B_k, g_k written to LDS in the solve kernel's staging layout.  xs / us: the state and input
+// (LDS); xf: scratch [N][12] (LDS).  Ends with a workgroup barrier.
+template <int NT>
+__device__ __forceinline__ void block_linearize(const VP& p, int N, double Ts, const double* xs, const double* us,
+                                                double* xf, double* A, double* Bm, double* g) {
+    const int t = threadIdx.x;
+    if (t < 64) {
+        // rollout (rollout_kernel's arithmetic): per stage, lanes 0 / 1 / 2 run the front-tire chain,
+        // the rear-tire chain and sincos(phi) as ONE instruction stream (atan2 -> atan -> sincos),
+        // the results are broadcast with v_readlane and every lane steps the (uniform) state
+        double x[6];
+        for (int i = 0; i < 6; ++i) x[i] = xs[i];
+        const double u0 = us[0], u1 = us[1];
+        double sd, cd;
+        sincos(u1, &sd, &cd);
+        const bool fr = (t == 0);
+        const double Bt = fr ? p.Bf : p.Br, Ct = fr ? p.Cf : p.Cr;
+        for (int k = 0; k < N; ++k) {
+            const double phi = x[2], vx = x[3], vy = x[4], omega = x[5];
+            const double avx = fabs(vx);
+            const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
+            const double vx_eff = np_sign(vx) * mx;
+            const double at = atan2(fr ? omega * p.lf + vy : omega * p.lr - vy, vx_eff);
+            const double alpha = clampd(fr ? -at + u1 : at, -p.maxAlpha, p.maxAlpha);
+            const double z = (t < 2) ? Ct * atan(Bt * alpha) : phi;
+            double sz, cz;
+            sincos(z, &sz, &cz);
+            const double Fy_f = p.Df * readlane_d(sz, 0), Fy_r = p.Dr * readlane_d(sz, 1);
+            const double sphi = readlane_d(sz, 2), cphi = readlane_d(cz, 2);
+            const double Frx = (p.Cm1 - p.Cm2 * vx) * u0 - p.Cr0 - p.Cr2 * (vx * vx);
+            double f[6];
+            f[0] = vx * cphi - vy * sphi;
+            f[1] = vx * sphi + vy * cphi;
+            f[2] = omega;
+            f[3] = (1.0 / p.m) * (Frx - Fy_f * sd + p.m * vy * omega);
+            f[4] = (1.0 / p.m) * (Fy_r + Fy_f * cd - p.m * vx * omega);
+            f[5] = (1.0 / p.Iz) * (Fy_f * p.lf * cd - Fy_r * p.lr);
+            if (t == 0)
+                for (int i = 0; i < 6; ++i) {
+                    xf[12 * k + i] = x[i];
+                    xf[12 * k + 6 + i] = f[i];
+                }
+            for (int i = 0; i < 6; ++i) x[i] = x[i] + Ts * f[i];
+        }
     }
+    __syncthreads();
+    const double d = us[0], de = us[1];
+    // vx / vy / omega columns: one (column, stage) per lane, one code path
+    for (int tau = t; tau < 3 * N; tau += NT) {
+        const int grp = tau / N, k = tau - grp * N;
+        double xb[6], J[6];
+        for (int i = 0; i < 6; ++i) xb[i] = xf[12 * k + i];
+        state_column(p, xb, d, de, grp, J);
+        const int cc = 3 + grp;
+        for (int r = 0; r < 6; ++r) A[36 * k + 6 * r + cc] = a_entry(r, cc, Ts, J[r]);
+    }
+    // phi / d / delta columns, the constant X, Y columns: one stage per lane
+    for (int k = t; k < N; k += NT) {
+        double xb[6], Jphi[6], Jd[6], Jde[6];
+        for (int i = 0; i < 6; ++i) xb[i] = xf[12 * k + i];
+        cheap_columns(p, xb, d, de, Jphi, Jd, Jde);
+        for (int r = 0; r < 6; ++r) {
+            A[36 * k + 6 * r + 0] = a_entry(r, 0, Ts, 0.0);
+            A[36 * k + 6 * r + 1] = a_entry(r, 1, Ts, 0.0);
+            A[36 * k + 6 * r + 2] = a_entry(r, 2, Ts, Jphi[r]);
+            Bm[12 * k + 2 * r + 0] = Ts * Jd[r];
+            Bm[12 * k + 2 * r + 1] = Ts * Jde[r];
+        }
+    }
+    __syncthreads();
+    for (int k = t; k < N; k += NT) {
+        double xb[6], fk[6], Ak[36], Bk[12], gk[6];
+        for (int i = 0; i < 6; ++i) { xb[i] = xf[12 * k + i]; fk[i] = xf[12 * k + 6 + i]; }
+        for (int i = 0; i < 36; ++i) Ak[i] = A[36 * k + i];
+        for (int i = 0; i < 12; ++i) Bk[i] = Bm[12 * k + i];
+        g_stage(Ak, Bk, xb, fk, d, de, Ts, gk);
+        for (int r = 0; r < 6; ++r) g[6 * k + r] = gk[r];
+    }
+    __syncthreads();
 }
 
 }  // namespace tgmpc

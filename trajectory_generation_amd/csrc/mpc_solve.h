@@ -17,6 +17,7 @@
 // Everything is float64, like the reference.
 #pragma once
 #include "mpc_common.h"
+#include "mpc_linearize.h"
 
 namespace tgmpc {
 
@@ -24,8 +25,8 @@ namespace tgmpc {
 // NN = capacity in QP variables (>= 2N); CLOSED = closed-loop step (window from the state, plant
 // update, history).  A_k, B_k, g_k are read from a.Ad / a.Bd / a.gd ([B,N,36], [B,N,12], [B,N,6]).
 // =====================================================================================
-template <int NN, bool CLOSED>
-__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(NN <= 64 ? 2 : 1))) void solve_kernel(const KArgs a) {
+template <int NN, bool CLOSED, bool FUSED = false>
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(NN <= 64 ? 2 : 1))) void solve_kernel(const KArgs a0) {
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
@@ -49,12 +50,25 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     __shared__ double s_red[16 * WAVES];
     __shared__ int s_flag[4];
 
+    // Fused closed loop (traj_closed_loop_run): nsteps steps of this instance in one launch -- the
+    // state, u_prev and the warm-start rho stay on chip and the linearization runs in the
+    // workgroup (block_linearize), so no instance waits for the slowest one of a step.  The whole
+    // body is the loop body, with the thread index passed through an opaque move each step so that
+    // nothing per-lane is hoisted out of the loop (it would stay live across the solve and spill).
+    constexpr bool fused = FUSED;
+    const int nsteps = FUSED ? a0.nsteps : 1;
+    double rho_carry = 0.0;
+    bool carry_ok = false;
+    for (int step = 0; step < nsteps; ++step) {
+    const KArgs& a = a0;
+    const int tstep = a.t + step;
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
     // closed loop: workgroups take instances longest-previous-solve first (LPT order), so the
     // slowest solves start at once instead of in the last dispatch round
     const int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
-    const int t = threadIdx.x;
+    int t = threadIdx.x;
+    if constexpr (FUSED) asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
     const int lane = t & 63, wid = t >> 6;
     const int N = c.N, n = 2 * N;
     const double Ts = c.Ts;
@@ -62,7 +76,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     const int kk = t >> 1, ch = t & 1;  // stage and channel of variable t
     int xb = 0;                         // rotating exchange buffer
     auto stamp = [&](int i, long long v) {
-        if (a.dbg && t == 0) a.dbg[(size_t)b * 16 + i] = v;
+        if (a.dbg && t == 0) a.dbg[(size_t)b * 32 + i] = v;
     };
     stamp(0, __builtin_amdgcn_s_memtime());
 
@@ -128,8 +142,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
     for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     if (CLOSED) {
-        if (t < 6) s_x0[t] = a.x_state[6 * b + t];
-        if (t < 2) s_up[t] = a.u_state[2 * b + t];
+        if (!fused || step == 0) {   // later fused steps: the previous step's plant update (LDS)
+            if (t < 6) s_x0[t] = a.x_state[6 * b + t];
+            if (t < 2) s_up[t] = a.u_state[2 * b + t];
+        }
     } else {
         if (t < 6) s_x0[t] = a.x0[6 * b + t];
         if (t < 2) s_up[t] = a.u_prev[2 * b + t];
@@ -173,7 +189,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     stamp(2, __builtin_amdgcn_s_memrealtime());   // 100 MHz wall clock (comparable across XCDs)
     // ---- 3. condensed QP (:180-250) --------------------------------------------------
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
-    if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
+    if (fused) {
+        // s_F (the condensing's F rows) is the rollout record's scratch here; zeroed again after
+        block_linearize<NT>(p, N, Ts, s_x0, s_up, s_F, s_big, s_big + 36 * N, s_big + 48 * N);
+        for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
+    } else if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
         // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
         // at once (one L2/MALL latency, no VGPRs); the three blocks are contiguous in s_big as double2
         // [A 18N | B 6N | g 3N].  Chunk r lands at s_big2[r NT + lane]; lanes past the end re-load
@@ -194,6 +214,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         for (int i = t; i < 12 * N; i += NT) s_big[36 * N + i] = gB[i];
         for (int i = t; i < 6 * N; i += NT) s_big[48 * N + i] = gg[i];
     }
+    stamp(16, __builtin_amdgcn_s_memtime());
     const double* const cA = s_big;
     const double* const cB = s_big + 36 * N;
     const double* const cg = s_big + 48 * N;
@@ -205,6 +226,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         s_sc[2 * k + 1] = ck;
     }
     __syncthreads();
+    stamp(17, __builtin_amdgcn_s_memtime());
 
     // P = sum_k G_k' C_k' 2W C_k G_k and q = sum_k G_k' C_k' 2W e_k, accumulated stage by stage:
     // lane t carries column t of the input sensitivity G_k (6-vector); the free response xh_k and
@@ -227,8 +249,16 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     };
     {
         const double sw0 = sqrt(2.0 * c.q_c), sw1 = sqrt(2.0 * c.q_phi), sw2 = sqrt(2.0 * c.q_vx);
+        // FREE lane (a spare lane past the variables, when there is one) carries the free response
+        // xh as its "G column": the same A_k G FMAs every lane already issues, started from g_k
+        // (same operation order as a separate xh recursion, bit for bit); the other lanes read the
+        // four components they need back with v_readlane.
+        constexpr bool FREE_LANE = WAVES == 1 && NN < 64;   // v_readlane: same wave
+        constexpr int FL = NT - 1;
         double xh[6], G[6] = {0, 0, 0, 0, 0, 0};
         for (int i = 0; i < 6; ++i) xh[i] = s_x0[i];
+        if (FREE_LANE && t == FL)
+            for (int i = 0; i < 6; ++i) G[i] = s_x0[i];
         constexpr int NB = (NN + 15) / 16;          // 16-wide column blocks (MFMA path)
         constexpr int NTILE = NB * (NB + 1) / 2;
         constexpr int FS = 16 * NB;
@@ -244,26 +274,29 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         const int mr = (t >> 4) & 3, mc = t & 15;   // MFMA operand slot of this lane: k-row, column
         for (int k = 0; k < N; ++k) {
             const double* Ak = cA + 36 * k;
-            // free response xh_{k+1} = A_k xh_k + g_k (uniform)
-            double xn[6];
+            if constexpr (!FREE_LANE) {
+                // free response xh_{k+1} = A_k xh_k + g_k (uniform)
+                double xn[6];
 #pragma unroll
-            for (int r = 0; r < 6; ++r) {
-                double v = cg[6 * k + r];
+                for (int r = 0; r < 6; ++r) {
+                    double v = cg[6 * k + r];
 #pragma unroll
-                for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], xh[cc], v);
-                xn[r] = v;
+                    for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], xh[cc], v);
+                    xn[r] = v;
+                }
+#pragma unroll
+                for (int r = 0; r < 6; ++r) xh[r] = xn[r];
             }
-#pragma unroll
-            for (int r = 0; r < 6; ++r) xh[r] = xn[r];
             // input sensitivities: columns of inputs applied before stage k propagate, stage k's
             // inputs enter through B_k
             // (branch-free: every lane forms A_k G, then selects -- no divergent exec juggling)
             {
-                const bool prop = own && (t < 2 * k), enter = own && (kk == k);
+                const bool fl = FREE_LANE && t == FL;
+                const bool prop = (own && (t < 2 * k)) || fl, enter = own && (kk == k);
                 double Gn[6];
 #pragma unroll
                 for (int r = 0; r < 6; ++r) {
-                    double v = 0.0;
+                    double v = fl ? cg[6 * k + r] : 0.0;
 #pragma unroll
                     for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], G[cc], v);
                     const double bv = cB[12 * k + 2 * r + ch];
@@ -271,6 +304,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 }
 #pragma unroll
                 for (int r = 0; r < 6; ++r) G[r] = Gn[r];
+                if constexpr (FREE_LANE) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) xh[r] = readlane_d(G[r], FL);
+                }
             }
             // stage k+1 outputs: tracking errors of the free response, weighted sensitivities
             const int k1 = k + 1;
@@ -282,17 +319,27 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
             if constexpr (WAVES == 1) {
                 double* fb = s_F + (k & 1) * 4 * FS;    // 2 rotating slots; row 3 and columns >= n stay 0
+#ifdef TGMPC_EXP_NO_FSYNC
+                double opv[NB];
+#pragma unroll
+                for (int ib = 0; ib < NB; ++ib) opv[ib] = F0 + ib * F1 + F2;
+#else
                 if (own) { fb[t] = F0; fb[FS + t] = F1; fb[2 * FS + t] = F2; }
                 __syncthreads();
                 double opv[NB];
 #pragma unroll
                 for (int ib = 0; ib < NB; ++ib) opv[ib] = fb[mr * FS + 16 * ib + mc];
+#endif
                 int ti = 0;
 #pragma unroll
                 for (int ib = 0; ib < NB; ++ib)
 #pragma unroll
                     for (int jb = ib; jb < NB; ++jb, ++ti)
+#ifdef TGMPC_EXP_NO_MFMA
+                        acc[ti][0] += opv[ib] * opv[jb];
+#else
                         acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(opv[ib], opv[jb], acc[ti], 0, 0, 0);
+#endif
             } else {
                 double* buf = s_ex + (xb & 1) * 3 * NN;   // 2 rotating slots of 3*NN
                 xb++;
@@ -304,6 +351,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             }
         }
         __syncthreads();
+        stamp(18, __builtin_amdgcn_s_memtime());
         if constexpr (WAVES == 1) {
             // accumulator tiles (lane: row 16 ib + mr + 4 reg, column 16 jb + mc) -> packed P -> rows
             int ti = 0;
@@ -322,6 +370,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             for (int j = 0; j < NN; ++j) Prow[j] = own ? s_P[paddr(j, tt)] : 0.0;
         }
     }
+    stamp(19, __builtin_amdgcn_s_memtime());
     // input penalties U'RU and dU'Rd dU (dU_0 = U_0 - u_prev)
     double Rs[4], Rds[4];
     Rs[0] = c.R[0]; Rs[3] = c.R[3]; Rs[1] = Rs[2] = 0.5 * (c.R[1] + c.R[2]);
@@ -537,9 +586,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         // (iterates start at zero as cold; shifting the previous primal/dual point was measured to
         // lengthen the iteration tail).  mpc_6stati.py:256 asks OSQP for warm_start=True, a no-op
         // there because a new Problem is built every call; the polished optimum does not depend on rho.
-        if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {
-            const double* wv = a.wsWarm + 4 * (size_t)b;
-            if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
+        if (CLOSED && c.warm_start && tstep > 0) {
+            if (fused && step > 0) {
+                if (carry_ok) rho = fmin(fmax(rho_carry, RHO_MIN), RHO_MAX);
+            } else if (a.wsWarm) {
+                const double* wv = a.wsWarm + 4 * (size_t)b;
+                if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
+            }
         }
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
         Res r = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -880,6 +933,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         }
         if (iter > c.max_iter) iter = c.max_iter;
         xsol = cold(C_D) * x;
+        if (CLOSED) {
+            rho_carry = rho;
+            carry_ok = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
+        }
         if (CLOSED && a.wsWarm && t == 0) {
             const bool okst = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
             a.wsWarm[4 * (size_t)b] = rho;
@@ -896,6 +953,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     } else {
         status = early;
         iter = 0;
+        carry_ok = false;
         if (CLOSED && a.wsWarm && t == 0) {
             a.wsWarm[4 * (size_t)b + 1] = 0.0;
             a.wsWarm[4 * (size_t)b + 2] = 0.0;
@@ -910,10 +968,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     __syncthreads();
     if (own) Ubuf[t] = xsol;
     __syncthreads();
-    // X_opt by the linear model X_{k+1} = A_k X_k + B_k U_k + g_k (s_xh reused)
+    // X_opt by the linear model X_{k+1} = A_k X_k + B_k U_k + g_k (s_xh reused); the closed loop
+    // returns neither X_opt nor the objective (main.py:94 keeps only u_cmd): skipped there
     if (t < 6) s_xh[t] = s_x0[t];
     __syncthreads();
-    for (int k = 0; k < N; ++k) {
+    for (int k = 0; k < (CLOSED ? 0 : N); ++k) {
         if (t < 6) {
             double v = 0.0;
             for (int cc = 0; cc < 6; ++cc) v += gA[k * 36 + t * 6 + cc] * s_xh[6 * k + cc];
@@ -924,7 +983,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     }
     // objective = cost of :217-250 at (X_opt, U_opt)
     double op = 0.0;
-    for (int k = t; k <= N; k += NT) {
+    for (int k = t; k <= (CLOSED ? -1 : N); k += NT) {
         const double* X = s_xh + 6 * k;
         double s = s_sc[2 * k], co = s_sc[2 * k + 1];
         double ec = s * (X[0] - s_pref[3 * k]) - co * (X[1] - s_pref[3 * k + 1]);
@@ -939,7 +998,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             op += d0 * (c.Rd[0] * d0 + c.Rd[1] * d1) + d1 * (c.Rd[2] * d0 + c.Rd[3] * d1);
         }
     }
-    double obj = block_sum(op);
+    double obj = CLOSED ? 0.0 : block_sum(op);
     stamp(7, __builtin_amdgcn_s_memtime());
     stamp(3, __builtin_amdgcn_s_memrealtime());
     const double nan = __builtin_nan("");
@@ -953,18 +1012,22 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             for (int i = 0; i < 6; ++i) {
                 double xn = xs[i] + Ts * f[i];
                 a.x_state[6 * b + i] = xn;
-                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + a.t + 1) * 6 + i] = xn;
+                s_x0[i] = xn;
+                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + tstep + 1) * 6 + i] = xn;
             }
             a.u_state[2 * b] = uc0;
             a.u_state[2 * b + 1] = uc1;
+            s_up[0] = uc0;
+            s_up[1] = uc1;
             if (a.hist_u) {
-                a.hist_u[((size_t)b * a.hist_T + a.t) * 2] = uc0;
-                a.hist_u[((size_t)b * a.hist_T + a.t) * 2 + 1] = uc1;
+                a.hist_u[((size_t)b * a.hist_T + tstep) * 2] = uc0;
+                a.hist_u[((size_t)b * a.hist_T + tstep) * 2 + 1] = uc1;
             }
-            if (a.status) a.status[b] = status;
-            if (a.iters) a.iters[b] = iter;
+            if (a.status) a.status[(size_t)step * a.B + b] = status;
+            if (a.iters) a.iters[(size_t)step * a.B + b] = iter;
         }
-        return;
+        __syncthreads();
+        continue;
     }
     if (t == 0) {
         a.u_cmd[2 * b] = uc0;
@@ -981,6 +1044,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             a.X_opt[(size_t)b * 6 * (N + 1) + i] = good ? s_xh[6 * k + r] : nan;
         }
     }
+    }   // steps
 }
 
 }  // namespace tgmpc

@@ -473,4 +473,44 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     return e;
 }
 
+int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
+                         double* x, double* u_prev, const double* vref, int t0, int steps, int hist_T,
+                         double* hist_x, double* hist_u, int* status, int* iters, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+    if (!p || B < 0 || steps < 0 || !paths_ok(paths)) return TRAJ_E_ARG;
+    int e = check_cfg(c);
+    if (e) return e;
+    if (B == 0 || steps == 0) return TRAJ_OK;
+    if (!x || !u_prev || !vref || t0 < 0) return TRAJ_E_ARG;
+    if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, c->N)) return TRAJ_E_ARG;
+    if ((hist_x || hist_u) && t0 + steps > hist_T) return TRAJ_E_ARG;
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.p = *p;
+    a.c = *c;
+    a.B = B;
+    a.vref = vref;
+    a.path = PathArgs{paths->kmax, paths->kind, paths->pc, paths->nk, paths->xk, paths->coef};
+    a.x_state = x;
+    a.u_state = u_prev;
+    a.t = t0;
+    a.hist_T = hist_T;
+    a.hist_x = hist_x;
+    a.hist_u = hist_u;
+    a.status = status;
+    a.iters = iters;
+    a.dbg = g_dbg;
+    a.nsteps = steps;
+    carve_workspace(a, workspace, B, c->N);
+    hipStream_t st = (hipStream_t)stream;
+    stamp(0, st);
+    stamp(1, st);
+    stamp(2, st);
+    stamp(3, st);
+    e = launch_mpc(a, st, 3);
+    stamp(4, st);
+    if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
+    return e;
+}
+
 }  // extern "C"
