@@ -33,6 +33,19 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
     print("phase       median      p90       max   (cycles)")
     for i, nm in enumerate(names):
         print(f"{nm:10s} {np.median(ph[:, i]):9.0f} {np.percentile(ph[:, i], 90):9.0f} {ph[:, i].max():9.0f}")
+    if fused:
+        # slot 22: first-step start (indexed by workgroup), 23: last-step end (by instance), 100 MHz
+        st0, en = d[:, 22].astype(float), d[:, 23].astype(float)
+        t0 = st0.min()
+        span = (en.max() - t0) / 100.0
+        busy = (en - st0[np.argsort(np.argsort(np.arange(B)))] ) if False else None
+        print("fused launch span %.1f us; workgroup starts: median %.1f p90 %.1f max %.1f us; instance ends: median %.1f"
+              " p90 %.1f max %.1f us" % (span, np.median(st0 - t0) / 100, np.percentile(st0 - t0, 90) / 100,
+                                         (st0.max() - t0) / 100, np.median(en - t0) / 100,
+                                         np.percentile(en - t0, 90) / 100, (en.max() - t0) / 100))
+        lin = np.diff(d[:, [1, 20, 21, 16]], axis=1)
+        for i, nm in enumerate(["  rollout", "  jac state columns", "  jac phi/d/delta + g"]):
+            print(f"{nm:22s} {np.median(lin[:, i]):9.0f} {np.percentile(lin[:, i], 90):9.0f}")
     sub = np.diff(d[:, [1, 16, 17, 18, 19, 4]], axis=1)
     for i, nm in enumerate(["  window/stage-issue", "  sincos+landed", "  stage loop", "  P rows", "  penalties"]):
         print(f"{nm:22s} {np.median(sub[:, i]):9.0f} {np.percentile(sub[:, i], 90):9.0f}")

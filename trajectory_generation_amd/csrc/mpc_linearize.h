@@ -243,8 +243,10 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 // (LDS); xf: scratch [N][12] (LDS).  Ends with a workgroup barrier.
 template <int NT>
 __device__ __forceinline__ void block_linearize(const VP& p, int N, double Ts, const double* xs, const double* us,
-                                                double* xf, double* A, double* Bm, double* g) {
+                                                double* xf, double* A, double* Bm, double* g,
+                                                long long* dbg = nullptr) {
     const int t = threadIdx.x;
+    auto mark = [&](int i) { if (dbg && t == 0) dbg[i] = __builtin_amdgcn_s_memtime(); };
     if (t < 64) {
         // rollout (rollout_kernel's arithmetic): per stage, lanes 0 / 1 / 2 run the front-tire chain,
         // the rear-tire chain and sincos(phi) as ONE instruction stream (atan2 -> atan -> sincos),
@@ -285,6 +287,7 @@ __device__ __forceinline__ void block_linearize(const VP& p, int N, double Ts, c
         }
     }
     __syncthreads();
+    mark(20);
     const double d = us[0], de = us[1];
     // vx / vy / omega columns: one (column, stage) per lane, one code path
     for (int tau = t; tau < 3 * N; tau += NT) {
@@ -295,6 +298,7 @@ __device__ __forceinline__ void block_linearize(const VP& p, int N, double Ts, c
         const int cc = 3 + grp;
         for (int r = 0; r < 6; ++r) A[36 * k + 6 * r + cc] = a_entry(r, cc, Ts, J[r]);
     }
+    mark(21);
     // phi / d / delta columns, the constant X, Y columns: one stage per lane
     for (int k = t; k < N; k += NT) {
         double xb[6], Jphi[6], Jd[6], Jde[6];

@@ -59,6 +59,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     const int nsteps = FUSED ? a0.nsteps : 1;
     double rho_carry = 0.0;
     bool carry_ok = false;
+    int iter_sum = 0;   // ADMM iterations over the launch (cost record for the next launch's order)
+    if (a0.dbg && threadIdx.x == 0) a0.dbg[(size_t)blockIdx.x * 32 + 22] = __builtin_amdgcn_s_memrealtime();
     for (int step = 0; step < nsteps; ++step) {
     const KArgs& a = a0;
     const int tstep = a.t + step;
@@ -191,7 +193,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
     if (fused) {
         // s_F (the condensing's F rows) is the rollout record's scratch here; zeroed again after
-        block_linearize<NT>(p, N, Ts, s_x0, s_up, s_F, s_big, s_big + 36 * N, s_big + 48 * N);
+        block_linearize<NT>(p, N, Ts, s_x0, s_up, s_F, s_big, s_big + 36 * N, s_big + 48 * N,
+                            a.dbg ? a.dbg + (size_t)b * 32 : nullptr);
         for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     } else if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
         // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
@@ -1025,6 +1028,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             }
             if (a.status) a.status[(size_t)step * a.B + b] = status;
             if (a.iters) a.iters[(size_t)step * a.B + b] = iter;
+            iter_sum += iter;
+            if (a.wsWarm && step == nsteps - 1) a.wsWarm[4 * (size_t)b + 3] = (double)iter_sum / nsteps;
+            if (step == nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // fused: launch span
         }
         __syncthreads();
         continue;

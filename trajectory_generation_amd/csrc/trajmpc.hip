@@ -128,9 +128,10 @@ __global__ void ref_window_kernel(PathArgs pa, int B, int N, double Ts, const do
 }
 
 // ---------------------------------------------------------------- closed-loop solve order
-// Counting sort of the instances by their previous ADMM iteration count (25-iteration buckets,
-// descending): a permutation whatever the workspace holds (non-finite keys land in bucket 0).
-__global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, int* perm) {
+// Counting sort of the instances by a per-instance cost record (ADMM iterations: slot 2 = the last
+// step's, slot 3 = the mean per step of the last fused launch; 25-iteration buckets, descending): a
+// permutation whatever the workspace holds (non-finite keys land in bucket 0).
+__global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, int* perm, int slot) {
     constexpr int NBK = 512;
     __shared__ int hist[NBK];
     __shared__ int offs[NBK];
@@ -138,7 +139,7 @@ __global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, 
     for (int i = t; i < NBK; i += 1024) hist[i] = 0;
     __syncthreads();
     auto key = [&](int i) -> int {
-        const double v = fmin(fmax(warm[4 * (size_t)i + 2] / 25.0, 0.0), (double)(NBK - 1));
+        const double v = fmin(fmax(warm[4 * (size_t)i + slot] / 25.0, 0.0), (double)(NBK - 1));
         return (int)v;
     };
     for (int i = t; i < B; i += 1024) atomicAdd(&hist[key(i)], 1);
@@ -463,7 +464,7 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     if (t > 0) {
         // order this step's solves by the previous step's iteration counts (longest first)
         int* perm = (int*)(a.wsWarm + (size_t)B * 4);
-        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, (const double*)a.wsWarm, B, perm);
+        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, (const double*)a.wsWarm, B, perm, 2);
         a.perm = perm;
     }
     stamp(3, st);
@@ -506,6 +507,13 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     stamp(0, st);
     stamp(1, st);
     stamp(2, st);
+    if (t0 > 0) {
+        // longest-first over the whole launch: instances ordered by their mean ADMM iterations per
+        // step in the previous launch, so the slowest trajectories are dispatched in the first round
+        int* perm = (int*)(a.wsWarm + (size_t)B * 4);
+        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, (const double*)a.wsWarm, B, perm, 3);
+        a.perm = perm;
+    }
     stamp(3, st);
     e = launch_mpc(a, st, 3);
     stamp(4, st);
