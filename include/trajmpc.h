@@ -113,8 +113,8 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
 /* Device workspace the MPC step needs for B instances of horizon N: the linearization A_k, B_k, g_k
  * handed from the linearize kernels to the solve kernel (B * N * 54 doubles), the rollout record
  * (x_k, f_k) per stage (B * N * 12 doubles), then the closed-loop record of the previous step
- * (B * 4 doubles: rho, valid flag, ADMM iterations) and the closed-loop solve order (B ints,
- * longest previous solve first).  Pass the same buffer to every traj_closed_loop_step of one run;
+ * (B * 4 doubles: rho, valid flag, ADMM iterations, mean iterations of the last fused run), the
+ * closed-loop solve order (B ints, longest first) and the fused run's step queue (B + 2 ints).  Pass the same buffer to every traj_closed_loop_step of one run;
  * step t = 0 starts cold. */
 size_t traj_mpc_workspace_bytes(int B, int N);
 
@@ -189,6 +189,9 @@ int traj_debug_set_stamps(long long* buf);
  * traj_debug_kernel_times synchronizes, returns the mean milliseconds per step of the four kernels
  * in ms[4] and the number of timed steps, and restarts the count.  For bench.py's roofline leg. */
 int traj_debug_kernel_timing(int max_steps);
+/* traj_closed_loop_run's grid: the resident workgroup slots of the device (0, default) or the given
+ * count (at least ceil(B / 8)); each workgroup runs its instances step by step.  For tests. */
+int traj_debug_fused_grid(int workgroups);
 int traj_debug_kernel_times(double* ms, int* n_steps);
 
 #ifdef __cplusplus

@@ -358,6 +358,15 @@ def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
     TB.closed_loop_run(x, u, paths, vr, cfg, None, 10, T - 10, hx, hu, st[10:], it[10:])
     assert torch.equal(hx, per["X"]) and torch.equal(hu, per["U"])
     assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"])
+    # several instances per workgroup (a grid smaller than B), with the heavy/light rank pairing
+    from trajectory_generation_amd import _lib
+    try:
+        _lib.check(_lib.lib().traj_debug_fused_grid(28), "traj_debug_fused_grid")
+        fus2 = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    finally:
+        _lib.lib().traj_debug_fused_grid(0)
+    for k in ("X", "U", "status", "iters"):
+        assert torch.equal(per[k], fus2[k]), k
 
 
 # ------------------------------------------------------------------ drop-in module

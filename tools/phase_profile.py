@@ -43,6 +43,7 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
               " p90 %.1f max %.1f us" % (span, np.median(st0 - t0) / 100, np.percentile(st0 - t0, 90) / 100,
                                          (st0.max() - t0) / 100, np.median(en - t0) / 100,
                                          np.percentile(en - t0, 90) / 100, (en.max() - t0) / 100))
+        print("workgroups started within 20 us of the first: %d (resident capacity)" % int(((st0 - t0) < 2000).sum()))
         lin = np.diff(d[:, [1, 20, 21, 16]], axis=1)
         for i, nm in enumerate(["  rollout", "  jac state columns", "  jac phi/d/delta + g"]):
             print(f"{nm:22s} {np.median(lin[:, i]):9.0f} {np.percentile(lin[:, i], 90):9.0f}")

@@ -95,6 +95,7 @@ _SIGS = {
     "traj_ref_window_batch": (C.c_int, [C.POINTER(Paths), C.c_int, C.c_int, C.c_double, _V, _V, _V, _V]),
     "traj_debug_set_stamps": (C.c_int, [_V]),
     "traj_debug_kernel_timing": (C.c_int, [C.c_int]),
+    "traj_debug_fused_grid": (C.c_int, [C.c_int]),
     "traj_debug_kernel_times": (C.c_int, [_V, _V]),
     "traj_knet_prior_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float, C.c_int,
                                       _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),

@@ -40,6 +40,9 @@ struct PathArgs {
     const double* coef;
 };
 
+// fused closed loop: instances per workgroup at most (the grid is the resident workgroups, or more)
+#define TRAJ_FUSED_MAX_PER_WG 8
+
 struct KArgs {
     traj_vehicle_params p;
     traj_mpc_config c;
@@ -73,6 +76,8 @@ struct KArgs {
     double* wsWarm;          // closed loop: per instance [rho, valid, ADMM iterations, 0] of the previous step
     const int* perm;         // closed loop: instance order (longest previous solve first), or null
     int nsteps;              // > 0: fused closed loop, nsteps steps per launch (status / iters [nsteps, B])
+    int fused_grid;          // fused: workgroups to launch (0: the resident slots; traj_debug_fused_grid)
+    int* queue;              // fused: [0] next work item, [1] error flag, [2 + b] completed steps of b
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

@@ -35,6 +35,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     __shared__ double s_pref[3 * (NM + 1)];
     __shared__ double s_vref[NM + 1];
     __shared__ double s_x0[6], s_up[2];
+    __shared__ int s_item;
     // one region, two lives: A_k, B_k, g_k of every stage staged for the condensing, then (once P
     // is formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values
     constexpr int NLIN = 54 * NM;
@@ -56,19 +57,50 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // body is the loop body, with the thread index passed through an opaque move each step so that
     // nothing per-lane is hoisted out of the loop (it would stay live across the solve and spill).
     constexpr bool fused = FUSED;
-    const int nsteps = FUSED ? a0.nsteps : 1;
-    double rho_carry = 0.0;
-    bool carry_ok = false;
-    int iter_sum = 0;   // ADMM iterations over the launch (cost record for the next launch's order)
-    if (a0.dbg && threadIdx.x == 0) a0.dbg[(size_t)blockIdx.x * 32 + 22] = __builtin_amdgcn_s_memrealtime();
-    for (int step = 0; step < nsteps; ++step) {
+    // fused: the grid is the resident workgroups; each takes work items (step, rank) from a queue in
+    // order -- all ranks of step 0, then of step 1, ... (rank = the previous launch's cost order) --
+    // and waits, if it must, until the instance's previous step is complete.  The instance state
+    // (x, u_prev, warm-start record) passes between workgroups through global memory with agent-scope
+    // release / acquire on the per-instance step counter, so a slow solve delays only its instance
+    // and every slot stays busy until the queue is drained.
+    bool more = true;
+    for (int step = 0; more; ++step) {
     const KArgs& a = a0;
+    int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
+    if constexpr (FUSED) {
+        __syncthreads();
+        if (threadIdx.x == 0) s_item = atomicAdd(&a.queue[0], 1);
+        __syncthreads();
+        const int q = s_item;
+        if (q >= a.B * a.nsteps) break;
+        step = q / a.B;
+        const int rank = q - step * a.B;
+        b = a.perm ? a.perm[rank] : rank;
+        if (threadIdx.x == 0 && step > 0) {
+            int spins = 0;
+            while (__hip_atomic_load(&a.queue[2 + b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < step) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1 << 22)) {   // bounded: a lost hand-off is reported, never a hang
+                    __hip_atomic_store(&a.queue[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (a.dbg && threadIdx.x == 0 && step == 0) {   // diagnostics: start, HW_ID, XCC_ID
+            unsigned hw, xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            a.dbg[(size_t)b * 32 + 22] = __builtin_amdgcn_s_memrealtime();
+            a.dbg[(size_t)b * 32 + 24] = hw;
+            a.dbg[(size_t)b * 32 + 25] = xcc;
+        }
+    } else {
+        more = false;
+    }
     const int tstep = a.t + step;
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
-    // closed loop: workgroups take instances longest-previous-solve first (LPT order), so the
-    // slowest solves start at once instead of in the last dispatch round
-    const int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
     int t = threadIdx.x;
     if constexpr (FUSED) asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
     const int lane = t & 63, wid = t >> 6;
@@ -144,10 +176,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
     for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     if (CLOSED) {
-        if (!fused || step == 0) {   // later fused steps: the previous step's plant update (LDS)
-            if (t < 6) s_x0[t] = a.x_state[6 * b + t];
-            if (t < 2) s_up[t] = a.u_state[2 * b + t];
-        }
+        if (t < 6) s_x0[t] = a.x_state[6 * b + t];
+        if (t < 2) s_up[t] = a.u_state[2 * b + t];
     } else {
         if (t < 6) s_x0[t] = a.x0[6 * b + t];
         if (t < 2) s_up[t] = a.u_prev[2 * b + t];
@@ -590,9 +620,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         // lengthen the iteration tail).  mpc_6stati.py:256 asks OSQP for warm_start=True, a no-op
         // there because a new Problem is built every call; the polished optimum does not depend on rho.
         if (CLOSED && c.warm_start && tstep > 0) {
-            if (fused && step > 0) {
-                if (carry_ok) rho = fmin(fmax(rho_carry, RHO_MIN), RHO_MAX);
-            } else if (a.wsWarm) {
+            if (a.wsWarm) {
                 const double* wv = a.wsWarm + 4 * (size_t)b;
                 if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
             }
@@ -936,10 +964,6 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         }
         if (iter > c.max_iter) iter = c.max_iter;
         xsol = cold(C_D) * x;
-        if (CLOSED) {
-            rho_carry = rho;
-            carry_ok = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
-        }
         if (CLOSED && a.wsWarm && t == 0) {
             const bool okst = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
             a.wsWarm[4 * (size_t)b] = rho;
@@ -956,7 +980,6 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     } else {
         status = early;
         iter = 0;
-        carry_ok = false;
         if (CLOSED && a.wsWarm && t == 0) {
             a.wsWarm[4 * (size_t)b + 1] = 0.0;
             a.wsWarm[4 * (size_t)b + 2] = 0.0;
@@ -1015,22 +1038,28 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             for (int i = 0; i < 6; ++i) {
                 double xn = xs[i] + Ts * f[i];
                 a.x_state[6 * b + i] = xn;
-                s_x0[i] = xn;
                 if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + tstep + 1) * 6 + i] = xn;
             }
             a.u_state[2 * b] = uc0;
             a.u_state[2 * b + 1] = uc1;
-            s_up[0] = uc0;
-            s_up[1] = uc1;
+
             if (a.hist_u) {
                 a.hist_u[((size_t)b * a.hist_T + tstep) * 2] = uc0;
                 a.hist_u[((size_t)b * a.hist_T + tstep) * 2 + 1] = uc1;
             }
             if (a.status) a.status[(size_t)step * a.B + b] = status;
             if (a.iters) a.iters[(size_t)step * a.B + b] = iter;
-            iter_sum += iter;
-            if (a.wsWarm && step == nsteps - 1) a.wsWarm[4 * (size_t)b + 3] = (double)iter_sum / nsteps;
-            if (step == nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // fused: launch span
+            if (FUSED) {
+                // mean iterations per step of this launch (the next launch's order), accumulated
+                if (a.wsWarm) {
+                    double* m = a.wsWarm + 4 * (size_t)b + 3;
+                    const double acc = (step == 0 ? 0.0 : *m) + iter;
+                    *m = (step == a.nsteps - 1) ? acc / a.nsteps : acc;
+                }
+                if (step == a.nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // launch span
+                // hand the instance to whichever workgroup takes its next step
+                __hip_atomic_store(&a.queue[2 + b], step + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         __syncthreads();
         continue;
@@ -1050,7 +1079,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             a.X_opt[(size_t)b * 6 * (N + 1) + i] = good ? s_xh[6 * k + r] : nan;
         }
     }
-    }   // steps
+    }   // steps / work items
 }
 
 }  // namespace tgmpc

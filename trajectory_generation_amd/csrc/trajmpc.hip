@@ -210,6 +210,7 @@ static int check_cfg(const traj_mpc_config* c) {
 }
 
 static long long* g_dbg = nullptr;  // diagnostics buffer (traj_debug_set_stamps)
+static int g_fused_grid = 0;        // traj_debug_fused_grid
 
 // per-kernel timing of traj_closed_loop_step (traj_debug_kernel_timing): 5 events per step bracket
 // rollout | jac | order | solve on the launch stream
@@ -231,6 +232,12 @@ int traj_abi_version(void) { return TRAJMPC_ABI_VERSION; }
 
 int traj_debug_set_stamps(long long* buf) {
     g_dbg = buf;
+    return TRAJ_OK;
+}
+
+int traj_debug_fused_grid(int workgroups) {
+    if (workgroups < 0) return TRAJ_E_ARG;
+    g_fused_grid = workgroups;
     return TRAJ_OK;
 }
 
@@ -391,8 +398,10 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
     if (B < 0 || N < 0) return 0;
-    // A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order (1 int)
-    return ((size_t)B * (size_t)N * 66 + (size_t)B * 4) * sizeof(double) + (((size_t)B * sizeof(int) + 7) & ~(size_t)7);
+    // A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order
+    // (1 int), fused-run step queue (counter, error flag, completed steps per instance)
+    return ((size_t)B * (size_t)N * 66 + (size_t)B * 4) * sizeof(double) +
+           ((((size_t)B * 2 + 2) * sizeof(int) + 7) & ~(size_t)7);
 }
 
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
@@ -502,14 +511,18 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.iters = iters;
     a.dbg = g_dbg;
     a.nsteps = steps;
+    a.fused_grid = g_fused_grid;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
+    // step queue: [0] next work item, [1] error flag, [2 + b] steps of instance b completed
+    a.queue = (int*)(a.wsWarm + (size_t)B * 4) + B;
+    if (hipMemsetAsync(a.queue, 0, ((size_t)B + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
     stamp(0, st);
     stamp(1, st);
     stamp(2, st);
     if (t0 > 0) {
-        // longest-first over the whole launch: instances ordered by their mean ADMM iterations per
-        // step in the previous launch, so the slowest trajectories are dispatched in the first round
+        // instances ranked by their mean ADMM iterations per step in the previous launch; the kernel
+        // pairs ranks heavy-with-light on each workgroup
         int* perm = (int*)(a.wsWarm + (size_t)B * 4);
         hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, (const double*)a.wsWarm, B, perm, 3);
         a.perm = perm;
