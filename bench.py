@@ -1,11 +1,13 @@
 """bench.py -- MPC steps/sec on B parallel spline-tracking trajectories (BASELINE.json configs[1]).
 
 One bench step = one closed-loop step of MPC/main.py:85-101 for all B trajectories of this rank
-(reference window -> mpc_step -> Euler plant) = one traj_closed_loop_step call = four HIP launches
-(rollout_kernel: nominal rollout; jac_kernel: FD Jacobians -> A, B, g; order_kernel: longest-first
-solve order; solve_kernel: window, condensing, ADMM + polish, plant, history).  Inputs and state are
-resident in HBM for the whole timed region.  The roofline object is solve_kernel's (the dominant
-kernel), timed with HIP events the library records on the launch stream around each kernel.
+(reference window -> linearization -> mpc_step -> Euler plant).  Default: the K timed steps run as ONE
+fused traj_closed_loop_run launch (resident workgroups take (step, trajectory) items from a queue;
+rollout, Jacobians, condensing, ADMM + polish and the plant update of an item inside one workgroup),
+bit-identical to K traj_closed_loop_step calls; --per-step times those calls instead (four launches
+per step: rollout_kernel, jac_kernel, order_kernel, solve_kernel).  Inputs and state are resident in
+HBM for the whole timed region.  The roofline object is solve_kernel's (the dominant / only kernel),
+timed with HIP events the library records on the launch stream.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 20] [--dt 0.05]
   N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...

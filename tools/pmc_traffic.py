@@ -23,6 +23,23 @@ def expected_blocks(batch, horizon):
             "solve_kernel": batch}
 
 
+def read_counter_fused(d, name):
+    """Fused closed loop: the largest solve_kernel<.., true, true> dispatch (the timed K-step launch)."""
+    vals = defaultdict(float)
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") == name and "solve_kernel" in row.get("Kernel_Name", "") \
+                        and "true, true" in row.get("Kernel_Name", ""):
+                    vals[row.get("Dispatch_Id")] += float(row["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no fused solve_kernel dispatch in {d}")
+    return max(vals.values())
+
+
 def read_counter(d, name, batch, horizon):
     want = expected_blocks(batch, horizon)
     vals = defaultdict(list)
@@ -56,7 +73,23 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--fused-steps", type=int, default=0,
+                    help="fused closed loop (bench default): K steps per launch; report that launch")
     a = ap.parse_args()
+    if a.fused_steps:
+        kib = 1024.0
+        fb = 2.0 * read_counter_fused(a.fetch, "FETCH_SIZE") * kib
+        wb = read_counter_fused(a.write, "WRITE_SIZE") * kib
+        res = {"batch": a.batch, "horizon": a.horizon, "fused": True, "steps_per_launch": a.fused_steps,
+               "fetch_bytes_per_launch": {"solve_kernel": fb}, "write_bytes_per_launch": {"solve_kernel": wb},
+               "hbm_bytes_per_kernel": {"solve_kernel": fb + wb}, "hbm_bytes_per_launch": fb + wb,
+               "hbm_bytes_per_step": (fb + wb) / a.fused_steps,
+               "note": "fused traj_closed_loop_run launch of fused_steps steps; FETCH_SIZE x2 (gfx950 correction), "
+                       "KiB -> bytes"}
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res, indent=1))
+        return
     fetch, nf = read_counter(a.fetch, "FETCH_SIZE", a.batch, a.horizon)
     write, nw = read_counter(a.write, "WRITE_SIZE", a.batch, a.horizon)
     kib = 1024.0
