@@ -99,15 +99,21 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50):
     u = (0.2 * torch.randn((B, 2, T), generator=g)).to(dev)
     m1x0 = (0.5 * torch.randn((B, 6, 1), generator=g)).to(dev)
     run = K.KNetSequenceRunner(model, B)
-    run.run(y, u, m1x0)                  # capture + warm
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    run.run(y, u, m1x0)
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+
+    def timed(**kw):
+        run.run(y, u, m1x0, **kw)        # capture + warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run.run(y, u, m1x0, **kw)
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    dt = timed(fused=True)               # the throughput path: 4 launches per step, T steps in one graph
+    dt_step_graph = timed(fused=False)   # module-level step (per-layer launches), one-step graph
     achieved = KNET_FLOP_PER_SEQ_STEP * B * T / dt / 1e12
     out = {"metric": f"KalmanNet seq/s (B={B}, T={T})", "value": B / dt, "unit": "sequences/s",
-           "ms_per_step": 1e3 * dt / T, "dtype": "f32",
+           "ms_per_step": 1e3 * dt / T, "dtype": "f32", "path": "fused (KNetSequenceRunner.run(fused=True))",
+           "module_step_graph_value": B / dt_step_graph,
            "config": {"workload": "KalmanNetNN inference (in_mult 5, out_mult 40, hidden 128), random-init weights, "
                                   "synthetic normalized inputs", "batch": B, "T": T, "Ts": 0.01},
            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",

@@ -11,6 +11,7 @@
  *   vehicle_model.py:19-79,109-153 f (clamps, Euler), h     kalman_net.py:161-162)
  *   torch.nn.GRU cell (seq_len 1), gates r, z, n            traj_knet_gru_gates_f32
  *   kalman_net.py:169-178 KNet_step posterior update        traj_knet_update_f32
+ *   kalman_net.py:145-216 whole step (throughput path)     traj_knet_front_f32 + traj_knet_fc2_f32 + traj_knet_back_f32
  *   (no reference counterpart) EKF baseline of config 5     traj_ekf_run_f64
  *
  * Conventions as trajmpc.h: device pointers, row-major, asynchronous on `stream`, 0 / TRAJ_E_*.
@@ -54,6 +55,55 @@ int traj_knet_gru_gates_f32(int B, int H, const float* gi, const float* gh, cons
  * KG [B,6,5] row-major (the reshape of FC2's output), dy [B,5], innov_logit: device scalar. */
 int traj_knet_update_f32(int B, const float* x_prior, const float* KG, const float* dy, const float* innov_logit,
                          float* x_post, void* stream);
+
+/* Fused step (throughput path): the weights of a KalmanNetNN (NNBuild with hidden_dim_gru = 128) as
+ * device pointers, row-major like the state_dict (nn.Linear weight [out, in]; nn.GRU weight_ih_l0
+ * [3H, in], weight_hh_l0 [3H, H], gates in torch order r, z, n). */
+typedef struct {
+    int m, n, hidden;              /* 6, 5, 128 */
+    int d_fc5, d_fc1, d_fc7, d_fc3; /* FC5 / FC1 / FC7 / FC3 widths: m*in_mult, n*n, n, m*m (all <= 64) */
+    const float *fc5_w, *fc5_b;                                    /* FC5.0 */
+    const float *gru_q_wih, *gru_q_bih, *gru_q_whh, *gru_q_bhh;    /* GRU_Q */
+    const float *gru_sigma_wih, *gru_sigma_bih, *gru_sigma_whh, *gru_sigma_bhh;   /* GRU_Sigma */
+    const float *fc1_w, *fc1_b, *fc7_w, *fc7_b;                    /* FC1.0, FC7.0 */
+    const float *gru_s_wih, *gru_s_bih, *gru_s_whh, *gru_s_bhh;    /* GRU_S */
+    const float *fc3_w, *fc3_b, *fc4_w, *fc4_b;                    /* FC3.0, FC4.0 */
+    const float* innov_logit;                                      /* scalar */
+    int d_fc2h;                                                    /* FC2 hidden width 2H*out_mult (multiple of 128) */
+    const float *fc2a_w, *fc2a_b, *fc2b_w, *fc2b_b;                /* FC2.0 [d_fc2h, 2H], FC2.2 [n*m, d_fc2h] */
+} traj_knet_net;
+
+/* The fused kernels read the eleven weight matrices from a packed copy made once per set of weights:
+ * traj_knet_packed_bytes(net) bytes (0 for unsupported shapes), filled by traj_knet_pack_f32 on
+ * `stream` (16-byte aligned buffer; layout P[k4][j][4] = W[j][4 k4 + c], zero past K).  Biases and
+ * innov_logit are read through `net` itself, so its pointers must stay valid while the kernels run. */
+size_t traj_knet_packed_bytes(const traj_knet_net* net);
+int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, void* stream);
+
+/* One KNet_step (kalman_net.py:145-216, eval mode) is three launches, front -> fc2 -> back:
+ *   front: prior (as traj_knet_prior_f32; u and y read with strides, e.g. column t of [B,2,T] /
+ *          [B,5,T]), FC5, GRU_Q, GRU_Sigma, FC1, FC7, GRU_S; updates h_q, h_s [B,H] in place and writes
+ *          x2 = [out_Sigma | h_S] [B,2H] (FC2's input), m1x_prior [B,m], dy [B,n];
+ *   fc2:   FC2 (Linear -> ReLU -> Linear) on x2 as partial sums over blocks of 128 hidden units into the
+ *          workspace ws (traj_knet_fc2_workspace_bytes(net, B) bytes), without materializing the
+ *          [B, d_fc2h] hidden activation;
+ *   back:  KG = FC2's output (bias + the partial sums in a fixed order; also written to KG_out [B, n*m]
+ *          if not NULL), FC3 on cat(h_S, KG), FC4 on cat(out_Sigma, FC3) -> h_sigma [B,H] (the new
+ *          h_Sigma), then x_post = m1x_prior + sigmoid(innov_logit) (KG dy); x_post is also written to
+ *          out[b*out_stride_b + i*out_stride_c] if out != NULL.
+ * TRAJ_E_UNSUPPORTED for shapes other than m=6, n=5, hidden=128 (FC5 / FC1+FC7 widths <= 32, FC3 <= 64,
+ * d_fc2h a multiple of 128).  Results are deterministic (no atomics). */
+int traj_knet_front_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts, const traj_knet_net* net,
+                        const float* packed, int B, const float* x_post, const float* u, int u_stride_b,
+                        int u_stride_c, const float* y, int y_stride_b, int y_stride_c, const float* x_mean,
+                        const float* x_std, const float* y_mean, const float* y_std, const float* u_mean,
+                        const float* u_std, float* h_q, const float* h_sigma, float* h_s, float* m1x_prior, float* dy,
+                        float* x2, void* stream);
+size_t traj_knet_fc2_workspace_bytes(const traj_knet_net* net, int B);
+int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* ws, size_t ws_bytes, void* stream);
+int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, const float* ws,
+                       const float* m1x_prior, const float* dy, float* h_sigma, float* x_post, float* out,
+                       int out_stride_b, int out_stride_c, float* KG_out, void* stream);
 
 /* Build-defined EKF baseline for config 5 ("MSE vs reference EKF"; the reference has no EKF, SURVEY.md
  * 8(f) f2), float64, one thread per sequence, all T steps in one launch:

@@ -96,6 +96,45 @@ def test_graph_runner_matches_eager_and_oracle(gpu):
     assert np.abs(eager - ref).max() <= 1e-3 * (1 + np.abs(ref).max())
 
 
+@pytest.mark.parametrize("B,T,groups", [(64, 30, 1), (7, 5, 1), (1, 3, 1), (37, 6, 3)])
+def test_fused_runner_vs_oracle(gpu, B, T, groups):
+    """Fused step (traj_knet_front_f32 / FC2 GEMMs / traj_knet_back_f32, whole-T graph) vs the CPU oracle,
+    ragged batches (B not a multiple of the 4 sequences a workgroup owns) included."""
+    from oracle import knet_oracle as KO
+    from trajectory_generation_amd.knet import KNetSequenceRunner
+    _, sysm, model = build(gpu, seed=1)
+    rng = np.random.default_rng(11 + B)
+    y = torch.tensor(rng.normal(size=(B, 5, T)), dtype=torch.float32, device=gpu)
+    u = torch.tensor(np.stack([rng.uniform(0, 0.5, (B, T)), rng.uniform(-0.3, 0.3, (B, T))], 1), dtype=torch.float32,
+                     device=gpu)
+    m1x0 = torch.tensor(rng.normal(size=(B, 6, 1)) * 0.5, dtype=torch.float32, device=gpu)
+    run = KNetSequenceRunner(model, B, groups=groups)
+    eager = run.run(y, u, m1x0, use_graph=False).cpu().numpy()
+    f0 = run.run(y, u, m1x0, use_graph=False, fused=True).cpu().numpy()
+    f1 = run.run(y, u, m1x0, fused=True).cpu().numpy()
+    f2 = run.run(y, u, m1x0, fused=True).cpu().numpy()       # graph replay
+    np.testing.assert_array_equal(f1, f0)
+    np.testing.assert_array_equal(f2, f0)
+    p = dict(KO.PARAMS)
+    p.update(LIMITS)
+    ref = KO.run_sequences(knet_weights(1), p, float(G["Ts"]), y.cpu().numpy(), u.cpu().numpy(), m1x0.cpu().numpy(),
+                           G["x_mean"], G["x_std"], G["y_mean"], G["y_std"]).numpy()
+    t = 1e-3 * (1 + np.abs(ref).max())
+    assert np.abs(f0 - ref).max() <= t
+    assert np.abs(f0 - eager).max() <= t
+
+
+def test_fused_runner_vs_reference_goldens(gpu):
+    from trajectory_generation_amd.knet import KNetSequenceRunner
+    _, _, model = build(gpu)
+    B = G["y_norm"].shape[0]
+    y = torch.tensor(G["y_norm"], dtype=torch.float32, device=gpu)
+    u = torch.tensor(G["u"], dtype=torch.float32, device=gpu)
+    m1x0 = torch.tensor(G["m1x0"], dtype=torch.float32, device=gpu)
+    post = KNetSequenceRunner(model, B).run(y, u, m1x0, fused=True).cpu().numpy()
+    assert np.abs(post - G["x_post"]).max() <= tol(G["x_post"])
+
+
 def test_ekf_vs_oracle_and_filters(gpu):
     """EKF baseline (f2): the GPU kernel equals the float64 oracle restatement, and it filters (lower
     state MSE than the raw measurements) on sequences simulated by the reference vehicle model."""

@@ -68,6 +68,16 @@ class KnetLimits(C.Structure):
         "omega_min", "omega_max")]
 
 
+class KnetNet(C.Structure):
+    """traj_knet_net (device pointers to a KalmanNetNN's weights, include/trajknet.h)."""
+    _fields_ = [(k, C.c_int) for k in ("m", "n", "hidden", "d_fc5", "d_fc1", "d_fc7", "d_fc3")] + [
+        (k, C.c_void_p) for k in (
+            "fc5_w", "fc5_b", "gru_q_wih", "gru_q_bih", "gru_q_whh", "gru_q_bhh", "gru_sigma_wih", "gru_sigma_bih",
+            "gru_sigma_whh", "gru_sigma_bhh", "fc1_w", "fc1_b", "fc7_w", "fc7_b", "gru_s_wih", "gru_s_bih",
+            "gru_s_whh", "gru_s_bhh", "fc3_w", "fc3_b", "fc4_w", "fc4_b", "innov_logit")] + [
+        ("d_fc2h", C.c_int)] + [(k, C.c_void_p) for k in ("fc2a_w", "fc2a_b", "fc2b_w", "fc2b_b")]
+
+
 class Paths(C.Structure):
     """traj_paths (closed-loop reference geometry per trajectory)."""
     _fields_ = [("kmax", C.c_int), ("kind", _V), ("pc", _V), ("nk", _V), ("xk", _V), ("coef", _V)]
@@ -101,6 +111,15 @@ _SIGS = {
                                       _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_knet_gru_gates_f32": (C.c_int, [C.c_int, C.c_int, _V, _V, _V, _V, _V]),
     "traj_knet_update_f32": (C.c_int, [C.c_int, _V, _V, _V, _V, _V, _V]),
+    "traj_knet_packed_bytes": (C.c_size_t, [C.POINTER(KnetNet)]),
+    "traj_knet_pack_f32": (C.c_int, [C.POINTER(KnetNet), _V, C.c_size_t, _V]),
+    "traj_knet_front_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float,
+                                      C.POINTER(KnetNet), _V, C.c_int, _V, _V, C.c_int, C.c_int, _V, C.c_int,
+                                      C.c_int, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+    "traj_knet_fc2_workspace_bytes": (C.c_size_t, [C.POINTER(KnetNet), C.c_int]),
+    "traj_knet_fc2_f32": (C.c_int, [C.POINTER(KnetNet), C.c_int, _V, _V, C.c_size_t, _V]),
+    "traj_knet_back_f32": (C.c_int, [C.POINTER(KnetNet), _V, C.c_int, _V, _V, _V, _V, _V, _V, _V, C.c_int,
+                                     C.c_int, _V, _V]),
     "traj_ekf_run_f64": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_double, C.c_int, C.c_int,
                                    _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,

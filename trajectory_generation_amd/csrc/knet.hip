@@ -22,19 +22,14 @@ struct KP {   // vehicle parameters rounded to float32
     float Cm1, Cm2, Cr0, Cr2, Br, Cr, Dr, Bf, Cf, Df, m, Iz, lf, lr, maxAlpha, vx_zero;
 };
 
-__global__ __launch_bounds__(256) void knet_prior_kernel(KP p, traj_knet_limits L, float Ts, int B,
-                                                         const float* __restrict__ x_post, const float* __restrict__ u,
-                                                         const float* __restrict__ y, const float* __restrict__ xm,
-                                                         const float* __restrict__ xs, const float* __restrict__ ym,
-                                                         const float* __restrict__ ys, const float* __restrict__ um,
-                                                         const float* __restrict__ us, float* __restrict__ m1x_prior,
-                                                         float* __restrict__ m1y, float* __restrict__ dy) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
+// kalman_net.py:145-162 for one sequence: x_post (normalized) -> prior (normalized), m1y, dy = y - m1y
+__device__ __forceinline__ void prior_one(const KP& p, const traj_knet_limits& L, float Ts, const float* xp, float d,
+                                          float delta, const float* yv, int ystride, const float* xm,
+                                          const float* xs, const float* ym, const float* ys, const float* um,
+                                          const float* us, float* prior, float* m1y, float* dyo) {
     float x[6];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) x[i] = __fadd_rn(__fmul_rn(x_post[6 * b + i], xs[i]), xm[i]);   // _denorm_x
-    float d = u[2 * b], delta = u[2 * b + 1];
+    for (int i = 0; i < 6; ++i) x[i] = __fadd_rn(__fmul_rn(xp[i], xs[i]), xm[i]);   // _denorm_x
     if (um && us) {   // _denorm_u (only when u statistics were set)
         d = __fadd_rn(__fmul_rn(d, us[0]), um[0]);
         delta = __fadd_rn(__fmul_rn(delta, us[1]), um[1]);
@@ -70,14 +65,27 @@ __global__ __launch_bounds__(256) void knet_prior_kernel(KP p, traj_knet_limits 
     for (int i = 0; i < 6; ++i) xn[i] = clampf_(__fadd_rn(x[i], __fmul_rn(Ts, xd[i])), lo[i], hi[i]);
     // renormalize; h = rows 0,1,3,4,5 (:136-153)
 #pragma unroll
-    for (int i = 0; i < 6; ++i) m1x_prior[6 * b + i] = __fdiv_rn(__fsub_rn(xn[i], xm[i]), xs[i]);
+    for (int i = 0; i < 6; ++i) prior[i] = __fdiv_rn(__fsub_rn(xn[i], xm[i]), xs[i]);
     const int hr[5] = {0, 1, 3, 4, 5};
 #pragma unroll
     for (int j = 0; j < 5; ++j) {
         const float my = __fdiv_rn(__fsub_rn(xn[hr[j]], ym[j]), ys[j]);
-        m1y[5 * b + j] = my;
-        if (dy) dy[5 * b + j] = __fsub_rn(y[5 * b + j], my);
+        if (m1y) m1y[j] = my;
+        if (dyo) dyo[j] = __fsub_rn(yv[j * ystride], my);
     }
+}
+
+__global__ __launch_bounds__(256) void knet_prior_kernel(KP p, traj_knet_limits L, float Ts, int B,
+                                                         const float* __restrict__ x_post, const float* __restrict__ u,
+                                                         const float* __restrict__ y, const float* __restrict__ xm,
+                                                         const float* __restrict__ xs, const float* __restrict__ ym,
+                                                         const float* __restrict__ ys, const float* __restrict__ um,
+                                                         const float* __restrict__ us, float* __restrict__ m1x_prior,
+                                                         float* __restrict__ m1y, float* __restrict__ dy) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    prior_one(p, L, Ts, x_post + 6 * b, u[2 * b], u[2 * b + 1], y ? y + 5 * b : nullptr, 1, xm, xs, ym, ys, um, us,
+              m1x_prior + 6 * b, m1y + 5 * b, dy ? dy + 5 * b : nullptr);
 }
 
 __device__ __forceinline__ float sigmoidf_(float v) { return 1.0f / (1.0f + expf(-v)); }
@@ -113,6 +121,424 @@ __global__ __launch_bounds__(256) void knet_update_kernel(int B, const float* __
 #pragma unroll
         for (int j = 0; j < 5; ++j) s = __fadd_rn(s, __fmul_rn(K[5 * i + j], e[j]));
         xo[6 * b + i] = __fadd_rn(xp[6 * b + i], __fmul_rn(gamma, s));
+    }
+}
+
+// ---------------------------------------------------------------- fused step (throughput path)
+// One KalmanNet step in two kernels around FC2 (kalman_net.py:145-216, eval mode):
+//   front: prior -> FC5 -> GRU_Q -> GRU_Sigma -> FC1, FC7 -> GRU_S, writing x2 = [out_Sigma | h_S]
+//          (FC2's input) and the hidden states;
+//   back:  FC3 -> FC4 (the new h_Sigma) -> posterior update, from FC2's output KG.
+// A workgroup owns KS sequences through every layer (no cross-workgroup dependency); activations stay
+// in LDS, weights stream from L2 in the packed layout P[k4][j][4] = W[j][4 k4 + c] (zero past K), so
+// the lanes of a wave (consecutive outputs j) read one contiguous 1 KiB run per float4 load.  GRU
+// cells: a thread per hidden unit and half of the sequences forms the six gate dot products and
+// applies torch's GRU gate math (as knet_gru_kernel).  Every dot product is a k-ordered fmaf chain
+// started at the bias: float32 results within rounding of the library GEMM path.
+constexpr int KS = 4;        // sequences per workgroup
+constexpr int KH = 128;      // hidden size (hidden_dim_gru)
+constexpr int KT = 256;      // threads per workgroup
+
+struct KNet {
+    int m, n, dFC5, dFC1, dFC7, dFC3;
+    const float *b5, *biQ, *bhQ, *biG, *bhG, *b1, *b7, *biS, *bhS, *b3, *b4, *logit, *b2b;
+    const float4 *W5, *WiQ, *WhQ, *WiG, *WhG, *W1, *W7, *WiS, *WhS, *W3, *W4;   // packed
+};
+
+// packed rows of 4 k per matrix: K rounded up to a multiple of 32 (zero weights past K), so that each
+// half of a split dot product runs a whole number of KD-row prefetch groups
+__host__ __device__ inline int k4_(int K) { return ((K + 31) / 32) * 8; }
+
+// Packed-buffer offsets (in floats) of the eleven matrices, in the order of traj_knet_net.
+struct PackPlan {
+    int N[11], K[11];
+    size_t off[12];
+};
+static PackPlan pack_plan(const traj_knet_net* w) {
+    PackPlan pl{};
+    const int H = w->hidden;
+    const int N[11] = {w->d_fc5, 3 * H, 3 * H, 3 * H, 3 * H, w->d_fc1, w->d_fc7, 3 * H, 3 * H, w->d_fc3, H};
+    const int K[11] = {w->m, w->d_fc5, H, H, H, H, w->n, w->d_fc1 + w->d_fc7, H, H + w->n * w->m, H + w->d_fc3};
+    pl.off[0] = 0;
+    for (int i = 0; i < 11; ++i) {
+        pl.N[i] = N[i];
+        pl.K[i] = K[i];
+        pl.off[i + 1] = pl.off[i] + (size_t)4 * k4_(K[i]) * N[i];
+    }
+    return pl;
+}
+
+__global__ void knet_pack_kernel(const float* __restrict__ W, int N, int K, float* __restrict__ P) {
+    const int K4 = k4_(K);
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)K4 * N * 4) return;
+    const int c = (int)(i & 3), j = (int)((i >> 2) % N), k4 = (int)((i >> 2) / N);
+    const int k = 4 * k4 + c;
+    P[i] = k < K ? W[(size_t)j * K + k] : 0.0f;
+}
+
+// Activations live in LDS k-major, xT[k][KS] (one float4 = the KS sequences' k-th input), rows
+// zero-padded to a multiple of 4.  Dot products are split over K between the two halves of the
+// workgroup (thread t: output / hidden unit t & 127, K half t >> 7) and the halves' partial sums are
+// added through LDS; weight loads run KD float4 rows ahead of the FMAs (one wave per SIMD here, so
+// the L2 latency must be covered inside the wave).
+constexpr int KD = 4;
+
+// acc[g][s] += sum_{k4 in [k4b, k4e)} xT[4 k4 + c][s] * P[k4][j + g * KH][c]  (P rows: NR per k4)
+template <int G>
+__device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const float4* __restrict__ P, int NR, int j,
+                                       float (&acc)[G][KS]) {
+    // k4e - k4b is a multiple of KD (k4_ padding); loads past the range are clamped, not skipped, so the
+    // loop has no divergent branches around its loads
+    float4 wb[KD][G];
+#pragma unroll
+    for (int d = 0; d < KD; ++d)
+#pragma unroll
+        for (int g = 0; g < G; ++g) wb[d][g] = P[(size_t)(k4b + d) * NR + j + g * KH];
+    for (int k4 = k4b; k4 < k4e; k4 += KD) {
+#pragma unroll
+        for (int d = 0; d < KD; ++d) {
+            const int kk = k4 + d;
+            const float4* xr = reinterpret_cast<const float4*>(xT + 4 * KS * kk);
+            const float4 x0 = xr[0], x1 = xr[1], x2 = xr[2], x3 = xr[3];   // k = 4kk .. 4kk+3, KS seqs each
+            float4 w[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) w[g] = wb[d][g];
+            const int kn = min(kk + KD, k4e - 1);
+#pragma unroll
+            for (int g = 0; g < G; ++g) wb[d][g] = P[(size_t)kn * NR + j + g * KH];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                acc[g][0] = fmaf(x3.x, w[g].w, fmaf(x2.x, w[g].z, fmaf(x1.x, w[g].y, fmaf(x0.x, w[g].x, acc[g][0]))));
+                acc[g][1] = fmaf(x3.y, w[g].w, fmaf(x2.y, w[g].z, fmaf(x1.y, w[g].y, fmaf(x0.y, w[g].x, acc[g][1]))));
+                acc[g][2] = fmaf(x3.z, w[g].w, fmaf(x2.z, w[g].z, fmaf(x1.z, w[g].y, fmaf(x0.z, w[g].x, acc[g][2]))));
+                acc[g][3] = fmaf(x3.w, w[g].w, fmaf(x2.w, w[g].z, fmaf(x1.w, w[g].y, fmaf(x0.w, w[g].x, acc[g][3]))));
+            }
+        }
+    }
+}
+
+// Dense layer: outT[j][s] = act(b[j] + sum_k xT[k][s] W[j][k]) for j < N <= KH (outT: LDS, k-major).
+// xch: LDS scratch of KH * KS floats.  Called by every thread of the workgroup.
+__device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* __restrict__ P,
+                                         const float* __restrict__ bias, int N, float* outT, bool relu, float* xch,
+                                         int t) {
+    const int j = t & (KH - 1), half = t >> 7, h2 = K4 >> 1;
+    float acc[1][KS] = {{0.0f, 0.0f, 0.0f, 0.0f}};
+    if (j < N) {
+        if (half == 0) acc[0][0] = acc[0][1] = acc[0][2] = acc[0][3] = bias[j];
+        dot_ks<1>(xT, half * h2, (half + 1) * h2, P, N, j, acc);
+        if (half) *reinterpret_cast<float4*>(xch + KS * j) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+    }
+    __syncthreads();
+    if (j < N && half == 0) {
+        const float4 o = *reinterpret_cast<const float4*>(xch + KS * j);
+        float4 r = make_float4(__fadd_rn(acc[0][0], o.x), __fadd_rn(acc[0][1], o.y), __fadd_rn(acc[0][2], o.z),
+                               __fadd_rn(acc[0][3], o.w));
+        if (relu) r = make_float4(fmaxf(r.x, 0.0f), fmaxf(r.y, 0.0f), fmaxf(r.z, 0.0f), fmaxf(r.w, 0.0f));
+        *reinterpret_cast<float4*>(outT + KS * j) = r;
+    }
+    __syncthreads();
+}
+
+// GRU cell (torch.nn.GRU, one layer, one step) for the KS sequences: xT [K][KS], hT [KH][KS] -> houtT.
+// Half 0 finishes sequences 0, 1 and half 1 sequences 2, 3.  xch: LDS scratch of 2 * KH * 12 floats.
+__device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT, const float4* __restrict__ Wi,
+                                       const float* __restrict__ bi, const float4* __restrict__ Wh,
+                                       const float* __restrict__ bh, float* houtT, float* xch, int t) {
+    const int u = t & (KH - 1), half = t >> 7;
+    float gi[3][KS], gh[3][KS];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int q = 0; q < KS; ++q) {
+            gi[g][q] = half ? 0.0f : bi[g * KH + u];
+            gh[g][q] = half ? 0.0f : bh[g * KH + u];
+        }
+    const int hi = K4 >> 1;
+    dot_ks<3>(xT, half * hi, (half + 1) * hi, Wi, 3 * KH, u, gi);
+    dot_ks<3>(hT, half * (KH / 8), (half + 1) * (KH / 8), Wh, 3 * KH, u, gh);
+    // hand the other half its two sequences' partial sums
+    float* mine = xch + (size_t)(half * KH + u) * 12;
+    const int so = half ? 0 : 2;   // the sequences the other half finishes
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        mine[4 * g + 0] = gi[g][so];
+        mine[4 * g + 1] = gi[g][so + 1];
+        mine[4 * g + 2] = gh[g][so];
+        mine[4 * g + 3] = gh[g][so + 1];
+    }
+    __syncthreads();
+    const float* other = xch + (size_t)((1 - half) * KH + u) * 12;
+    const int s0 = half ? 2 : 0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        float ir[3], hr[3];
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            ir[g] = __fadd_rn(gi[g][s0 + q], other[4 * g + q]);
+            hr[g] = __fadd_rn(gh[g][s0 + q], other[4 * g + 2 + q]);
+        }
+        // ATen GRUCell: r = sigmoid(h_r + i_r), z = sigmoid(h_z + i_z), n = tanh(i_n + h_n * r), h' = (h - n) z + n
+        const float r = sigmoidf_(__fadd_rn(hr[0], ir[0]));
+        const float z = sigmoidf_(__fadd_rn(hr[1], ir[1]));
+        const float nn = tanhf(__fadd_rn(ir[2], __fmul_rn(hr[2], r)));
+        const float hv = hT[u * KS + s0 + q];
+        houtT[u * KS + s0 + q] = __fadd_rn(__fmul_rn(__fsub_rn(hv, nn), z), nn);
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(KT) void knet_front_kernel(KP p, traj_knet_limits L, float Ts, KNet net, int B,
+                                                        const float* __restrict__ x_post, const float* __restrict__ u,
+                                                        int u_sb, int u_sc, const float* __restrict__ y, int y_sb,
+                                                        int y_sc, const float* __restrict__ xm,
+                                                        const float* __restrict__ xs, const float* __restrict__ ym,
+                                                        const float* __restrict__ ys, const float* __restrict__ um,
+                                                        const float* __restrict__ us, float* hQ, const float* hSig,
+                                                        float* hS, float* prior, float* dy, float* x2) {
+    __shared__ __attribute__((aligned(16))) float s_h[3][KH * KS];   // h_Q, h_Sigma, h_S (inputs), k-major
+    __shared__ __attribute__((aligned(16))) float s_q[KH * KS];      // new h_Q
+    __shared__ __attribute__((aligned(16))) float s_g[KH * KS];      // out_Sigma
+    __shared__ __attribute__((aligned(16))) float s_hs[KH * KS];     // new h_S
+    __shared__ __attribute__((aligned(16))) float s_pr[32 * KS];     // prior, zero-padded
+    __shared__ __attribute__((aligned(16))) float s_dy[32 * KS];     // innovation, zero-padded
+    __shared__ __attribute__((aligned(16))) float s_o5[32 * KS];     // FC5 output, zero-padded
+    __shared__ __attribute__((aligned(16))) float s_c1[32 * KS];     // [FC1 | FC7], zero-padded
+    __shared__ __attribute__((aligned(16))) float s_x[2 * KH * 12];  // half-sum exchange
+    const int t = threadIdx.x, b0 = blockIdx.x * KS;
+    const int nb = min(KS, B - b0);
+    for (int i = t; i < 3 * KS * KH; i += KT) {   // coalesced row reads -> k-major LDS
+        const int w = i / (KS * KH), r = i - w * KS * KH, s = r / KH, k = r - s * KH;
+        const float* src = (w == 0) ? hQ : (w == 1 ? hSig : hS);
+        s_h[w][k * KS + s] = (s < nb) ? src[(size_t)(b0 + s) * KH + k] : 0.0f;
+    }
+    if (t < 32 * KS) s_o5[t] = s_c1[t] = s_pr[t] = s_dy[t] = 0.0f;
+    __syncthreads();
+    if (t < KS) {
+        float pr[6] = {0, 0, 0, 0, 0, 0}, e[5] = {0, 0, 0, 0, 0};
+        if (t < nb) {
+            const int b = b0 + t;
+            prior_one(p, L, Ts, x_post + 6 * b, u[(size_t)b * u_sb], u[(size_t)b * u_sb + u_sc], y + (size_t)b * y_sb,
+                      y_sc, xm, xs, ym, ys, um, us, pr, nullptr, e);
+            for (int i = 0; i < 6; ++i) prior[6 * b + i] = pr[i];
+            for (int j = 0; j < 5; ++j) dy[5 * b + j] = e[j];
+        }
+        for (int i = 0; i < 6; ++i) s_pr[i * KS + t] = pr[i];
+        for (int j = 0; j < 5; ++j) s_dy[j * KS + t] = e[j];
+    }
+    __syncthreads();
+    dense_ks(s_pr, k4_(net.m), net.W5, net.b5, net.dFC5, s_o5, true, s_x, t);                    // FC5 + ReLU
+    gru_ks(s_o5, k4_(net.dFC5), s_h[0], net.WiQ, net.biQ, net.WhQ, net.bhQ, s_q, s_x, t);        // GRU_Q
+    gru_ks(s_q, KH / 4, s_h[1], net.WiG, net.biG, net.WhG, net.bhG, s_g, s_x, t);               // GRU_Sigma
+    dense_ks(s_g, KH / 4, net.W1, net.b1, net.dFC1, s_c1, true, s_x, t);                         // FC1 + ReLU
+    dense_ks(s_dy, k4_(net.n), net.W7, net.b7, net.dFC7, s_c1 + KS * net.dFC1, true, s_x, t);    // FC7 + ReLU
+    gru_ks(s_c1, k4_(net.dFC1 + net.dFC7), s_h[2], net.WiS, net.biS, net.WhS, net.bhS, s_hs, s_x, t);   // GRU_S
+    for (int i = t; i < nb * KH; i += KT) {
+        const int s = i / KH, k = i - s * KH;
+        const size_t b = (size_t)(b0 + s);
+        hQ[b * KH + k] = s_q[k * KS + s];
+        hS[b * KH + k] = s_hs[k * KS + s];
+        x2[b * 2 * KH + k] = s_g[k * KS + s];
+        x2[b * 2 * KH + KH + k] = s_hs[k * KS + s];
+    }
+}
+
+// FC2 = Linear(2H, dH) -> ReLU -> Linear(dH, n m) (kalman_net.py:88-95) without the [B, dH] hidden
+// activation ever reaching memory.  Workgroup (slab, bblk) owns 64 sequences x 256 hidden units:
+//   1. the x2 tile [64][2H] is staged in LDS (rows padded to 260 floats: conflict-free b128 reads);
+//   2. hid = relu(x2 W2a_slab^T + b2a) on v_mfma_f32_32x32x2_f32: wave w owns hidden units 64w..64w+63
+//      and all 64 rows (2 x 2 tiles of 32 x 32, A from LDS, B = W2a rows streamed from L2 KD chunks ahead);
+//   3. hid goes to LDS over the x2 tile, then v_mfma_f32_16x16x4_f32 forms the slab's contribution to
+//      FC2's output, part[slab][b][0:32] = hid W2b_slab^T (columns >= n m are zero); wave w: rows 16w...
+// The back kernel adds b2b and the slabs in slab order (deterministic, no atomics).
+// K order inside the MFMAs: in chunk c (8 k), lane half g of a 32x32x2 step takes k = 8c + 4g + e for
+// the chunk's e-th step, so one float4 per operand feeds four steps.  Blocks are spread so the b-blocks
+// of a slab share an XCD (its W2a slab stays in that XCD's L2).
+constexpr int F2_BT = 64, F2_HT = 256, F2_LD = 2 * KH + 4;
+static_assert(F2_HT + 4 == F2_LD, "hid tile reuses the x2 tile's rows");
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void knet_fc2_kernel(int B, int dH, const float* __restrict__ x2,
+                                                       const float* __restrict__ W2a, const float* __restrict__ b2a,
+                                                       const float* __restrict__ W2b, int nout,
+                                                       float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the hid tile
+    const int nslab = dH / F2_HT, nbb = (B + F2_BT - 1) / F2_BT;
+    int slab, bblk;
+    const int i = blockIdx.x;
+    if ((nslab & 7) == 0) {
+        const int xcd = i & 7, local = i >> 3;
+        slab = (local / nbb) * 8 + xcd;
+        bblk = local % nbb;
+    } else {
+        slab = i / nbb;
+        bblk = i % nbb;
+    }
+    const int t = threadIdx.x, w = t >> 6, l = t & 63;
+    const int b0 = bblk * F2_BT, h0 = slab * F2_HT;
+    constexpr int K = 2 * KH;   // FC2 input width
+#pragma unroll
+    for (int it = 0; it < F2_BT * (K / 4) / 256; ++it) {   // coalesced: a row is 64 consecutive float4s
+        const int q = t + 256 * it, row = q / (K / 4), c4 = q - row * (K / 4);
+        const int bsrc = min(b0 + row, B - 1);           // rows past B: duplicates, never stored
+        *reinterpret_cast<float4*>(s_t + row * F2_LD + 4 * c4) =
+            reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
+    }
+    const int g = l >> 5, r = l & 31;
+    const float4* pw0 = reinterpret_cast<const float4*>(W2a + (size_t)(h0 + 64 * w + r) * K) + g;
+    const float4* pw1 = reinterpret_cast<const float4*>(W2a + (size_t)(h0 + 64 * w + 32 + r) * K) + g;
+    constexpr int NC = K / 8, PD = 4;   // chunks; chunks of W2a loads in flight ahead of the MFMAs
+    float4 q0[PD], q1[PD];
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+        q0[d] = pw0[2 * d];
+        q1[d] = pw1[2 * d];
+    }
+    __syncthreads();
+    f32x16 c00 = {}, c01 = {}, c10 = {}, c11 = {};   // c<b tile><h tile>
+    const float* xa = s_t + r * F2_LD + 4 * g;
+    const float* xb = s_t + (32 + r) * F2_LD + 4 * g;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const int d = c % PD;
+        const float4 w0 = q0[d], w1 = q1[d];
+        if (c + PD < NC) {
+            q0[d] = pw0[2 * (c + PD)];
+            q1[d] = pw1[2 * (c + PD)];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // keep the W2a prefetch ahead of this chunk's MFMAs
+        const float4 a0 = *reinterpret_cast<const float4*>(xa + 8 * c);
+        const float4 a1 = *reinterpret_cast<const float4*>(xb + 8 * c);
+        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, w0.x, c00, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, w0.x, c10, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, w1.x, c01, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, w1.x, c11, 0, 0, 0);
+        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, w0.y, c00, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, w0.y, c10, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, w1.y, c01, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, w1.y, c11, 0, 0, 0);
+        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, w0.z, c00, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, w0.z, c10, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, w1.z, c01, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, w1.z, c11, 0, 0, 0);
+        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, w0.w, c00, 0, 0, 0);
+        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, w0.w, c10, 0, 0, 0);
+        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, w1.w, c01, 0, 0, 0);
+        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, w1.w, c11, 0, 0, 0);
+    }
+    __syncthreads();   // every wave is done with the x2 tile
+    {
+        // C/D of 32x32: col = lane & 31 (hidden unit), row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5) (b)
+        const int hA = 64 * w + r, hB = hA + 32;
+        const float bA = b2a[h0 + hA], bB = b2a[h0 + hB];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int row = (q & 3) + 8 * (q >> 2) + 4 * g;
+            s_t[row * F2_LD + hA] = fmaxf(__fadd_rn(c00[q], bA), 0.0f);
+            s_t[(32 + row) * F2_LD + hA] = fmaxf(__fadd_rn(c10[q], bA), 0.0f);
+            s_t[row * F2_LD + hB] = fmaxf(__fadd_rn(c01[q], bB), 0.0f);
+            s_t[(32 + row) * F2_LD + hB] = fmaxf(__fadd_rn(c11[q], bB), 0.0f);
+        }
+    }
+    __syncthreads();
+    {
+        // wave w: b rows 16w..16w+15 x outputs 0..31 (two 16x16 tiles), K = the slab's 256 hidden units
+        const int g4 = l >> 4, r4 = l & 15;
+        const float* ph = s_t + (16 * w + r4) * F2_LD + 4 * g4;
+        const int j0 = r4, j1 = 16 + r4;
+        const float4* u0p = reinterpret_cast<const float4*>(W2b + (size_t)min(j0, nout - 1) * dH + h0) + g4;
+        const float4* u1p = reinterpret_cast<const float4*>(W2b + (size_t)min(j1, nout - 1) * dH + h0) + g4;
+        const float m0 = j0 < nout ? 1.0f : 0.0f, m1 = j1 < nout ? 1.0f : 0.0f;
+        f32x4 e0 = {}, e1 = {};
+#pragma unroll 4
+        for (int c = 0; c < F2_HT / 16; ++c) {
+            const float4 hv = *reinterpret_cast<const float4*>(ph + 16 * c);
+            float4 u0 = u0p[4 * c], u1 = u1p[4 * c];
+            u0.x *= m0; u0.y *= m0; u0.z *= m0; u0.w *= m0;
+            u1.x *= m1; u1.y *= m1; u1.z *= m1; u1.w *= m1;
+            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.x, u0.x, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.x, u1.x, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.y, u0.y, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.y, u1.y, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.z, u0.z, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.z, u1.z, e1, 0, 0, 0);
+            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.w, u0.w, e0, 0, 0, 0);
+            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.w, u1.w, e1, 0, 0, 0);
+        }
+        // C/D of 16x16: col = lane & 15 (output j), row = 4 (lane >> 4) + reg (b)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int b = b0 + 16 * w + 4 * g4 + q;
+            if (b < B) {
+                float* dst = part + ((size_t)slab * B + b) * 32;
+                dst[r4] = e0[q];
+                dst[16 + r4] = e1[q];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const float* __restrict__ x2,
+                                                       const float* __restrict__ part, int nslab,
+                                                       const float* __restrict__ prior, const float* __restrict__ dy,
+                                                       float* hSig, float* x_post, float* out, int o_sb, int o_sc,
+                                                       float* KG_out) {
+    __shared__ __attribute__((aligned(16))) float s_a[(KH + 32) * KS];    // [h_S | KG | 0]: FC3's input
+    __shared__ __attribute__((aligned(16))) float s_b[(KH + 64) * KS];    // [out_Sigma | FC3 | 0]: FC4's input
+    __shared__ __attribute__((aligned(16))) float s_o[KH * KS];           // FC4 output (new h_Sigma)
+    __shared__ __attribute__((aligned(16))) float s_x[2 * KH * 12];
+    __shared__ float s_red[KS][32][2];
+    const int t = threadIdx.x, b0 = blockIdx.x * KS;
+    const int nb = min(KS, B - b0);
+    const int nm = net.n * net.m;
+    for (int i = t; i < KS * 2 * KH; i += KT) {
+        const int s = i / (2 * KH), k = i - s * 2 * KH;
+        const float v = (s < nb) ? x2[(size_t)(b0 + s) * 2 * KH + k] : 0.0f;
+        if (k < KH) s_b[k * KS + s] = v;
+        else s_a[(k - KH) * KS + s] = v;
+    }
+    for (int i = t; i < 64 * KS; i += KT) s_b[KH * KS + i] = 0.0f;
+    {   // KG = b2b + sum over FC2's slabs: thread (s, j, parity) sums the even or odd slabs
+        const int s = t >> 6, j = (t >> 1) & 31, q = t & 1;
+        float a = 0.0f;
+        if (s < nb) {
+            const float* pp = part + ((size_t)b0 + s) * 32 + j;
+#pragma unroll 10
+            for (int sl = q; sl < nslab; sl += 2) a = __fadd_rn(a, pp[(size_t)sl * B * 32]);
+        }
+        s_red[s][j][q] = a;
+    }
+    __syncthreads();
+    if (t < KS * 32) {
+        const int s = t >> 5, j = t & 31;
+        float v = 0.0f;
+        if (j < nm && s < nb) {
+            v = __fadd_rn(net.b2b[j], __fadd_rn(s_red[s][j][0], s_red[s][j][1]));
+            if (KG_out) KG_out[(size_t)(b0 + s) * nm + j] = v;
+        }
+        s_a[(KH + j) * KS + s] = v;
+    }
+    __syncthreads();
+    // FC3 + ReLU on cat(h_S, out_FC2); FC4 + ReLU on cat(out_Sigma, out_FC3) = the new h_Sigma
+    dense_ks(s_a, k4_(KH + nm), net.W3, net.b3, net.dFC3, s_b + KH * KS, true, s_x, t);
+    dense_ks(s_b, k4_(KH + net.dFC3), net.W4, net.b4, KH, s_o, true, s_x, t);
+    for (int i = t; i < nb * KH; i += KT) {
+        const int s = i / KH, k = i - s * KH;
+        hSig[(size_t)(b0 + s) * KH + k] = s_o[k * KS + s];
+    }
+    if (t < nb) {   // posterior (kalman_net.py:169-178), as knet_update_kernel
+        const int b = b0 + t;
+        const float gamma = sigmoidf_(net.logit[0]);
+        for (int i = 0; i < net.m; ++i) {
+            float sacc = 0.0f;
+            for (int j = 0; j < net.n; ++j)
+                sacc = __fadd_rn(sacc, __fmul_rn(s_a[(KH + net.n * i + j) * KS + t], dy[5 * b + j]));
+            const float v = __fadd_rn(prior[6 * b + i], __fmul_rn(gamma, sacc));
+            x_post[6 * b + i] = v;
+            if (out) out[(size_t)b * o_sb + (size_t)i * o_sc] = v;
+        }
     }
 }
 
@@ -287,6 +713,96 @@ int traj_knet_update_f32(int B, const float* x_prior, const float* KG, const flo
     if (!x_prior || !KG || !dy || !innov_logit || !x_post) return TRAJ_E_ARG;
     hipLaunchKernelGGL(knet_update_kernel, dim3(nblk(B, 256)), dim3(256), 0, (hipStream_t)stream, B, x_prior, KG, dy,
                        innov_logit, x_post);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+static bool knet_ok(const traj_knet_net* w) {
+    return w && w->m == 6 && w->n == 5 && w->hidden == KH && w->d_fc5 > 0 && w->d_fc5 <= 32 && w->d_fc1 > 0 &&
+           w->d_fc7 > 0 && w->d_fc1 + w->d_fc7 <= 32 && w->d_fc3 > 0 && w->d_fc3 <= 64 && w->fc5_w && w->fc5_b &&
+           w->gru_q_wih && w->gru_q_bih && w->gru_q_whh && w->gru_q_bhh && w->gru_sigma_wih && w->gru_sigma_bih &&
+           w->gru_sigma_whh && w->gru_sigma_bhh && w->fc1_w && w->fc1_b && w->fc7_w && w->fc7_b && w->gru_s_wih &&
+           w->gru_s_bih && w->gru_s_whh && w->gru_s_bhh && w->fc3_w && w->fc3_b && w->fc4_w && w->fc4_b && w->innov_logit &&
+           w->d_fc2h > 0 && w->d_fc2h % F2_HT == 0 && w->fc2a_w && w->fc2a_b && w->fc2b_w && w->fc2b_b;
+}
+static KNet knet_args(const traj_knet_net* w, const float* packed) {
+    const PackPlan pl = pack_plan(w);
+    auto P = [&](int i) { return reinterpret_cast<const float4*>(packed + pl.off[i]); };
+    return KNet{w->m,     w->n,     w->d_fc5, w->d_fc1, w->d_fc7, w->d_fc3, w->fc5_b,  w->gru_q_bih, w->gru_q_bhh,
+                w->gru_sigma_bih, w->gru_sigma_bhh, w->fc1_b, w->fc7_b, w->gru_s_bih, w->gru_s_bhh, w->fc3_b,
+                w->fc4_b, w->innov_logit, w->fc2b_b, P(0), P(1), P(2), P(3), P(4), P(5), P(6), P(7), P(8), P(9), P(10)};
+}
+
+size_t traj_knet_packed_bytes(const traj_knet_net* net) {
+    if (!knet_ok(net)) return 0;
+    return pack_plan(net).off[11] * sizeof(float);
+}
+
+int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, void* stream) {
+    if (!net || !packed) return TRAJ_E_ARG;
+    if (!knet_ok(net)) return TRAJ_E_UNSUPPORTED;
+    const PackPlan pl = pack_plan(net);
+    if (bytes < pl.off[11] * sizeof(float) || ((uintptr_t)packed & 15)) return TRAJ_E_ARG;
+    const float* W[11] = {net->fc5_w, net->gru_q_wih, net->gru_q_whh, net->gru_sigma_wih, net->gru_sigma_whh,
+                          net->fc1_w, net->fc7_w,     net->gru_s_wih, net->gru_s_whh,     net->fc3_w,
+                          net->fc4_w};
+    for (int i = 0; i < 11; ++i) {
+        const long long n = (long long)(pl.off[i + 1] - pl.off[i]);
+        hipLaunchKernelGGL(knet_pack_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, W[i], pl.N[i],
+                           pl.K[i], packed + pl.off[i]);
+    }
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_knet_front_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts, const traj_knet_net* net,
+                        const float* packed, int B, const float* x_post, const float* u, int u_stride_b,
+                        int u_stride_c, const float* y, int y_stride_b, int y_stride_c, const float* x_mean,
+                        const float* x_std, const float* y_mean, const float* y_std, const float* u_mean,
+                        const float* u_std, float* h_q, const float* h_sigma, float* h_s, float* m1x_prior, float* dy,
+                        float* x2, void* stream) {
+    if (!p || !lim || B < 0) return TRAJ_E_ARG;
+    if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!packed || ((uintptr_t)packed & 15) || !x_post || !u || !y || !x_mean || !x_std || !y_mean || !y_std || !h_q ||
+        !h_sigma || !h_s || !m1x_prior || !dy || !x2)
+        return TRAJ_E_ARG;
+    KP k{(float)p->Cm1, (float)p->Cm2, (float)p->Cr0, (float)p->Cr2, (float)p->Br, (float)p->Cr, (float)p->Dr,
+         (float)p->Bf,  (float)p->Cf,  (float)p->Df,  (float)p->m,   (float)p->Iz, (float)p->lf, (float)p->lr,
+         (float)p->maxAlpha, (float)p->vx_zero};
+    hipLaunchKernelGGL(knet_front_kernel, dim3(nblk(B, KS)), dim3(KT), 0, (hipStream_t)stream, k, *lim, Ts,
+                       knet_args(net, packed), B, x_post, u, u_stride_b, u_stride_c, y, y_stride_b, y_stride_c, x_mean,
+                       x_std, y_mean, y_std, u_mean, u_std, h_q, h_sigma, h_s, m1x_prior, dy, x2);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+size_t traj_knet_fc2_workspace_bytes(const traj_knet_net* net, int B) {
+    if (!knet_ok(net) || B < 0) return 0;
+    return (size_t)(net->d_fc2h / F2_HT) * (size_t)B * 32 * sizeof(float);
+}
+
+int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* ws, size_t ws_bytes, void* stream) {
+    if (B < 0) return TRAJ_E_ARG;
+    if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!x2 || !ws || ws_bytes < traj_knet_fc2_workspace_bytes(net, B) || ((uintptr_t)x2 & 15) ||
+        ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2b_w & 15))
+        return TRAJ_E_ARG;
+    const int nslab = net->d_fc2h / F2_HT, nbb = nblk(B, F2_BT);
+    hipLaunchKernelGGL(knet_fc2_kernel, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2,
+                       net->fc2a_w, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, const float* ws,
+                       const float* m1x_prior, const float* dy, float* h_sigma, float* x_post, float* out,
+                       int out_stride_b, int out_stride_c, float* KG_out, void* stream) {
+    if (B < 0) return TRAJ_E_ARG;
+    if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!packed || ((uintptr_t)packed & 15) || !x2 || !ws || !m1x_prior || !dy || !h_sigma || !x_post)
+        return TRAJ_E_ARG;
+    hipLaunchKernelGGL(knet_back_kernel, dim3(nblk(B, KS)), dim3(KT), 0, (hipStream_t)stream, knet_args(net, packed),
+                       B, x2, ws, net->d_fc2h / F2_HT, m1x_prior, dy, h_sigma, x_post, out, out_stride_b,
+                       out_stride_c, KG_out);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 

@@ -11,7 +11,11 @@ its checkpoints load unchanged.  What runs on the device per step (kalman_net.py
 * ``traj_knet_gru_gates_f32`` (HIP) the three GRU cells' gate arithmetic after their two GEMMs;
 * ``traj_knet_update_f32`` (HIP) x_post = x_prior + sigmoid(innov_logit) * KG dy (:169-178).
 
-``KNetSequenceRunner`` captures one whole step in a HIP graph and replays it T times.
+``KNetSequenceRunner`` captures one whole step in a HIP graph and replays it T times; its fused mode
+(the throughput path) runs a step as three launches -- ``traj_knet_front_f32`` (prior + FC5 + the three
+GRU cells + FC1/FC7 for four sequences per workgroup), ``traj_knet_fc2_f32`` (FC2 on the f32 matrix
+cores, its [B, 10240] hidden activation kept on chip), ``traj_knet_back_f32`` (FC3 + FC4 + posterior
+update) -- and captures all T steps in one graph.
 There is no CPU path: the ops raise without the HIP library or a GPU.
 """
 from __future__ import annotations
@@ -248,14 +252,46 @@ class KalmanNetNN(nn.Module):
         return self.KNet_step(y.to(self.device, torch.float32), u.to(self.device, torch.float32))
 
 
+def net_struct(model: "KalmanNetNN") -> _lib.KnetNet:
+    """traj_knet_net of a built KalmanNetNN (weights must stay alive and in place while it is used;
+    the fused kernels read a packed copy of the matrices, made by traj_knet_pack_f32, and the biases here)."""
+    w = _lib.KnetNet()
+    w.m, w.n, w.hidden = model.m, model.n, model.d_hidden_Q
+    w.d_fc5, w.d_fc1, w.d_fc7, w.d_fc3 = model.d_output_FC5, model.d_output_FC1, model.d_output_FC7, model.d_output_FC3
+    mods = {"fc5": model.FC5[0], "fc1": model.FC1[0], "fc7": model.FC7[0], "fc3": model.FC3[0], "fc4": model.FC4[0]}
+    for k, lin in mods.items():
+        for t in (lin.weight, lin.bias):
+            if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+                raise ValueError(f"{k}: fused KNet step needs contiguous float32 device weights")
+        setattr(w, k + "_w", lin.weight.data_ptr())
+        setattr(w, k + "_b", lin.bias.data_ptr())
+    for k, g in {"gru_q": model.GRU_Q, "gru_sigma": model.GRU_Sigma, "gru_s": model.GRU_S}.items():
+        for a in ("wih", "bih", "whh", "bhh"):
+            t = getattr(g, {"wih": "weight_ih_l0", "bih": "bias_ih_l0", "whh": "weight_hh_l0", "bhh": "bias_hh_l0"}[a])
+            if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+                raise ValueError(f"{k}: fused KNet step needs contiguous float32 device weights")
+            setattr(w, f"{k}_{a}", t.data_ptr())
+    w.innov_logit = model.innov_logit.data_ptr()
+    w.d_fc2h = model.d_hidden_FC2
+    for k, lin in {"fc2a": model.FC2[0], "fc2b": model.FC2[2]}.items():
+        for t in (lin.weight, lin.bias):
+            if t.dtype != torch.float32 or not t.is_contiguous() or not t.is_cuda:
+                raise ValueError(f"{k}: fused KNet step needs contiguous float32 device weights")
+        setattr(w, k + "_w", lin.weight.data_ptr())
+        setattr(w, k + "_b", lin.bias.data_ptr())
+    return w
+
+
 class KNetSequenceRunner:
     """T steps of a KalmanNetNN (eval mode) for B sequences, one step captured in a HIP graph.
 
     Mirrors the inference loop of training_prediction.py:118-137 / test_vehicle.py:123-145:
     init_hidden_KNet, InitSequence(m1x0), then forward(y[:, :, t], u[:, :, t]) for t < T."""
 
-    def __init__(self, model: KalmanNetNN, B: int):
-        self.model, self.B = model, B
+    def __init__(self, model: KalmanNetNN, B: int, groups: int = 1):
+        """groups: the fused mode's sequences split into that many independent launch chains (graph
+        branches), so one group's latency-bound GRU kernels overlap another's FC2 on the matrix cores."""
+        self.model, self.B, self.groups = model, B, groups
         dev = model.device
         self.y = torch.zeros((B, model.n, 1), device=dev)
         self.u = torch.zeros((B, 2, 1), device=dev)
@@ -267,10 +303,106 @@ class KNetSequenceRunner:
         md.init_hidden_KNet()
         md.InitSequence(m1x0, 0)
 
+    # ---------- fused mode: three launches per step, all T steps in one graph ----------
+    def _fused_steps(self, T, steps, g):
+        """Enqueue `steps` fused steps of row group g (rows r0:r1) on the current stream."""
+        md, S = self.model, self.fs
+        L = _lib.lib()
+        xm, xs, ym, ys = S["norm"]
+        n, m, H = md.n, md.m, md.d_hidden_Q
+        r0, r1 = S["rows"][g]
+        Bg, ws = r1 - r0, S["ws"][g]
+        row = lambda key, width: C.c_void_p(S[key].data_ptr() + 4 * r0 * width)   # noqa: E731
+        net, pk = C.byref(S["net"]), _p(S["pk"])
+        for t in range(steps):
+            _lib.check(L.traj_knet_front_f32(
+                C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, row("post", m),
+                C.c_void_p(S["u"].data_ptr() + 4 * (r0 * 2 * T + t)), 2 * T, T,
+                C.c_void_p(S["y"].data_ptr() + 4 * (r0 * n * T + t)), n * T, T,
+                _p(xm), _p(xs), _p(ym), _p(ys), _p(S["um"]), _p(S["us"]), row("hQ", H), row("hSig", H), row("hS", H),
+                row("prior", m), row("dy", n), row("x2", 2 * H), _stream()), "traj_knet_front_f32")
+            _lib.check(L.traj_knet_fc2_f32(net, Bg, row("x2", 2 * H), _p(ws), ws.numel() * 4, _stream()),
+                       "traj_knet_fc2_f32")
+            _lib.check(L.traj_knet_back_f32(
+                net, pk, Bg, row("x2", 2 * H), _p(ws), row("prior", m), row("dy", n), row("hSig", H),
+                row("post", m), C.c_void_p(S["out"].data_ptr() + 4 * (r0 * m * T + t)), m * T, T, None, _stream()),
+                "traj_knet_back_f32")
+
+    def _enqueue_all(self, T, steps):
+        """All row groups' steps; groups > 1 run as independent chains on side streams (graph branches)."""
+        S = self.fs
+        if len(S["rows"]) == 1:
+            self._fused_steps(T, steps, 0)
+            return
+        main = torch.cuda.current_stream()
+        for g, st in enumerate(S["streams"]):
+            st.wait_stream(main)
+            with torch.cuda.stream(st):
+                self._fused_steps(T, steps, g)
+        for st in S["streams"]:
+            main.wait_stream(st)
+
+    def _run_fused(self, y_seq, u_seq, m1x0, use_graph):
+        md, B = self.model, self.B
+        dev, T, H = md.device, y_seq.shape[2], md.d_hidden_Q
+        L = _lib.lib()
+        if md.training:
+            raise ValueError("fused KNet step is inference only (model.eval())")
+        S = getattr(self, "fs", None)
+        if S is None or S["T"] != T:
+            xm, xs, ym, ys = (t.reshape(-1).contiguous() for t in md._norm_tensors())
+            um = None if md.u_mean is None else md.u_mean.reshape(-1).contiguous()
+            us = None if md.u_std is None else md.u_std.reshape(-1).contiguous()
+            z = lambda *sh: torch.zeros(sh, dtype=torch.float32, device=dev)   # noqa: E731
+            G = max(1, min(self.groups, B))
+            cuts = [B * g // G for g in range(G + 1)]
+            S = {"T": T, "p": params_struct(md.sys.Params), "lim": limits_struct(md.sys.Params), "net": net_struct(md),
+                 "norm": (xm, xs, ym, ys), "um": um, "us": us,
+                 "y": z(B, md.n, T), "u": z(B, 2, T), "out": z(B, md.m, T), "post": z(B, md.m),
+                 "hQ": z(B, H), "hSig": z(B, H), "hS": z(B, H), "prior": z(B, md.m), "dy": z(B, md.n),
+                 "x2": z(B, 2 * H), "graph": None, "rows": list(zip(cuts[:-1], cuts[1:])),
+                 "streams": [torch.cuda.Stream() for _ in range(G)] if G > 1 else []}
+            nbytes = L.traj_knet_packed_bytes(C.byref(S["net"]))
+            if nbytes == 0:
+                raise NotImplementedError("fused KNet step: unsupported network shape")
+            S["pk"] = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+            S["ws"] = [torch.empty(L.traj_knet_fc2_workspace_bytes(C.byref(S["net"]), r1 - r0) // 4,
+                                   dtype=torch.float32, device=dev) for r0, r1 in S["rows"]]
+            _lib.check(L.traj_knet_pack_f32(C.byref(S["net"]), _p(S["pk"]), nbytes, _stream()), "traj_knet_pack_f32")
+            self.fs = S
+
+        def reset():
+            S["y"].copy_(y_seq)
+            S["u"].copy_(u_seq)
+            for k in ("hQ", "hSig", "hS"):
+                S[k].zero_()
+            S["post"].copy_(m1x0.reshape(B, md.m))
+
+        reset()
+        if not use_graph:
+            self._enqueue_all(T, T)
+            return S["out"].clone()
+        if S["graph"] is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._enqueue_all(T, min(T, 2))   # warm up before capture
+            torch.cuda.current_stream().wait_stream(s)
+            reset()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._enqueue_all(T, T)
+            S["graph"] = g
+        S["graph"].replay()
+        return S["out"].clone()
+
     @torch.no_grad()
-    def run(self, y_seq, u_seq, m1x0, use_graph=True):
-        """y_seq [B,n,T] normalized, u_seq [B,2,T], m1x0 [B,m,1] -> posterior [B,m,T] (normalized)."""
+    def run(self, y_seq, u_seq, m1x0, use_graph=True, fused=False):
+        """y_seq [B,n,T] normalized, u_seq [B,2,T], m1x0 [B,m,1] -> posterior [B,m,T] (normalized).
+        fused=True: the throughput path (eval mode; module state attributes are not updated)."""
         md = self.model
+        if fused:
+            return self._run_fused(y_seq, u_seq, m1x0, use_graph)
         T = y_seq.shape[2]
         out = torch.empty((self.B, md.m, T), device=md.device)
         if not use_graph:
