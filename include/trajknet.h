@@ -69,7 +69,7 @@ typedef struct {
     const float *gru_s_wih, *gru_s_bih, *gru_s_whh, *gru_s_bhh;    /* GRU_S */
     const float *fc3_w, *fc3_b, *fc4_w, *fc4_b;                    /* FC3.0, FC4.0 */
     const float* innov_logit;                                      /* scalar */
-    int d_fc2h;                                                    /* FC2 hidden width 2H*out_mult (multiple of 128) */
+    int d_fc2h;                                                    /* FC2 hidden width 2H*out_mult (multiple of 256) */
     const float *fc2a_w, *fc2a_b, *fc2b_w, *fc2b_b;                /* FC2.0 [d_fc2h, 2H], FC2.2 [n*m, d_fc2h] */
 } traj_knet_net;
 
@@ -84,15 +84,15 @@ int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, vo
  *   front: prior (as traj_knet_prior_f32; u and y read with strides, e.g. column t of [B,2,T] /
  *          [B,5,T]), FC5, GRU_Q, GRU_Sigma, FC1, FC7, GRU_S; updates h_q, h_s [B,H] in place and writes
  *          x2 = [out_Sigma | h_S] [B,2H] (FC2's input), m1x_prior [B,m], dy [B,n];
- *   fc2:   FC2 (Linear -> ReLU -> Linear) on x2 as partial sums over blocks of 128 hidden units into the
- *          workspace ws (traj_knet_fc2_workspace_bytes(net, B) bytes), without materializing the
+ *   fc2:   FC2 (Linear -> ReLU -> Linear) on x2 as partial sums over blocks of 320 hidden units (256 when
+ *          d_fc2h is not a multiple of 320) into the workspace ws (traj_knet_fc2_workspace_bytes(net, B) bytes), without materializing the
  *          [B, d_fc2h] hidden activation;
  *   back:  KG = FC2's output (bias + the partial sums in a fixed order; also written to KG_out [B, n*m]
  *          if not NULL), FC3 on cat(h_S, KG), FC4 on cat(out_Sigma, FC3) -> h_sigma [B,H] (the new
  *          h_Sigma), then x_post = m1x_prior + sigmoid(innov_logit) (KG dy); x_post is also written to
  *          out[b*out_stride_b + i*out_stride_c] if out != NULL.
  * TRAJ_E_UNSUPPORTED for shapes other than m=6, n=5, hidden=128 (FC5 / FC1+FC7 widths <= 32, FC3 <= 64,
- * d_fc2h a multiple of 128).  Results are deterministic (no atomics). */
+ * d_fc2h a multiple of 256).  fc2a_w, fc2a_b and fc2b_w must be 16-byte aligned.  Results are deterministic (no atomics). */
 int traj_knet_front_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts, const traj_knet_net* net,
                         const float* packed, int B, const float* x_post, const float* u, int u_stride_b,
                         int u_stride_c, const float* y, int y_stride_b, int y_stride_c, const float* x_mean,

@@ -345,27 +345,40 @@ __global__ __launch_bounds__(KT) void knet_front_kernel(KP p, traj_knet_limits L
 }
 
 // FC2 = Linear(2H, dH) -> ReLU -> Linear(dH, n m) (kalman_net.py:88-95) without the [B, dH] hidden
-// activation ever reaching memory.  Workgroup (slab, bblk) owns 64 sequences x 256 hidden units:
-//   1. the x2 tile [64][2H] is staged in LDS (rows padded to 260 floats: conflict-free b128 reads);
-//   2. hid = relu(x2 W2a_slab^T + b2a) on v_mfma_f32_32x32x2_f32: wave w owns hidden units 64w..64w+63
-//      and all 64 rows (2 x 2 tiles of 32 x 32, A from LDS, B = W2a rows streamed from L2 KD chunks ahead);
-//   3. hid goes to LDS over the x2 tile, then v_mfma_f32_16x16x4_f32 forms the slab's contribution to
-//      FC2's output, part[slab][b][0:32] = hid W2b_slab^T (columns >= n m are zero); wave w: rows 16w...
-// The back kernel adds b2b and the slabs in slab order (deterministic, no atomics).
-// K order inside the MFMAs: in chunk c (8 k), lane half g of a 32x32x2 step takes k = 8c + 4g + e for
-// the chunk's e-th step, so one float4 per operand feeds four steps.  Blocks are spread so the b-blocks
-// of a slab share an XCD (its W2a slab stays in that XCD's L2).
-constexpr int F2_BT = 64, F2_HT = 256, F2_LD = 2 * KH + 4;
-static_assert(F2_HT + 4 == F2_LD, "hid tile reuses the x2 tile's rows");
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+// activation ever reaching memory.  Workgroup (slab, bblk) owns 64 sequences x HS = 64 NT hidden units
+// (NT = 5: 32 slabs x 16 b-blocks = 512 workgroups at B = 1024, two per CU, every SIMD the same work):
+//   1. the x2 tile [64][2H] is staged in LDS (rows padded to 260 floats);
+//   2. wave w forms the TRANSPOSED hidden tile hidT[h][b] = W2a[h,:] . x2[b,:] for its 16 NT hidden units
+//      and all 64 sequences on v_mfma_f32_16x16x4_f32 (exact f32): A = W2a rows streamed from L2 PD chunks
+//      ahead, B = the x2 tile from LDS; NT x 4 independent 16 x 16 accumulators;
+//   3. relu(hidT + b2a) stays in the accumulators and IS the B operand of the second product:
+//      lane (g = l >> 4, r = l & 15) holds hidT[4g + q][r] in register q, so MFMA step q contracts over
+//      h = 4g + q -- outT[j][b] = sum_h W2b[j][h] hidT[h][b] with no LDS round trip (rows j >= n m are
+//      zero weights);
+//   4. the four waves' outT partials are added through LDS in wave order and the workgroup writes
+//      part[slab][b][0:32].
+// The back kernel adds b2b and the slabs in slab order (deterministic, no atomics).  K order inside the
+// MFMAs: in chunk c (16 k), lane group g takes k = 16c + 4g + e at step e, so one float4 per operand
+// feeds four steps.  Blocks are spread so the b-blocks of a slab share an XCD (its W2a slab stays in
+// that XCD's L2).
+constexpr int F2_BT = 64, F2_LD = 2 * KH + 4, F2_RS = 68;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void knet_fc2_kernel(int B, int dH, const float* __restrict__ x2,
-                                                       const float* __restrict__ W2a, const float* __restrict__ b2a,
-                                                       const float* __restrict__ W2b, int nout,
-                                                       float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the hid tile
-    const int nslab = dH / F2_HT, nbb = (B + F2_BT - 1) / F2_BT;
+__device__ __forceinline__ float f4c(const float4& v, int e) {   // component e (constant after unrolling)
+    return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+}
+
+// hidden units per workgroup: 320 when dH allows (512 equal workgroups at B = 1024), else 256
+__host__ __device__ inline int fc2_slab(int dH) { return (dH % 320 == 0) ? 320 : 256; }
+
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2_kernel(
+    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const float* __restrict__ b2a,
+    const float* __restrict__ W2b, int nout, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the wave partials
+    static_assert(4 * 32 * F2_RS <= F2_BT * F2_LD, "partials fit the x2 tile");
+    constexpr int HS = 64 * NT;
+    const int nslab = dH / HS, nbb = (B + F2_BT - 1) / F2_BT;
     int slab, bblk;
     const int i = blockIdx.x;
     if ((nslab & 7) == 0) {
@@ -376,8 +389,8 @@ __global__ __launch_bounds__(256) void knet_fc2_kernel(int B, int dH, const floa
         slab = i / nbb;
         bblk = i % nbb;
     }
-    const int t = threadIdx.x, w = t >> 6, l = t & 63;
-    const int b0 = bblk * F2_BT, h0 = slab * F2_HT;
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
+    const int b0 = bblk * F2_BT, hw0 = slab * HS + 16 * NT * w;
     constexpr int K = 2 * KH;   // FC2 input width
 #pragma unroll
     for (int it = 0; it < F2_BT * (K / 4) / 256; ++it) {   // coalesced: a row is 64 consecutive float4s
@@ -386,96 +399,98 @@ __global__ __launch_bounds__(256) void knet_fc2_kernel(int B, int dH, const floa
         *reinterpret_cast<float4*>(s_t + row * F2_LD + 4 * c4) =
             reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
     }
-    const int g = l >> 5, r = l & 31;
-    const float4* pw0 = reinterpret_cast<const float4*>(W2a + (size_t)(h0 + 64 * w + r) * K) + g;
-    const float4* pw1 = reinterpret_cast<const float4*>(W2a + (size_t)(h0 + 64 * w + 32 + r) * K) + g;
-    constexpr int NC = K / 8, PD = 4;   // chunks; chunks of W2a loads in flight ahead of the MFMAs
-    float4 q0[PD], q1[PD];
+    const float* pa = W2a + (size_t)(hw0 + r) * K + 4 * g;   // h-tile ht: + 16 ht K; chunk c: + 16 c
+    constexpr int NC = K / 16, PD = 2;   // chunks; chunks of W2a loads in flight ahead of the MFMAs
+    float4 wa[PD][NT];
 #pragma unroll
-    for (int d = 0; d < PD; ++d) {
-        q0[d] = pw0[2 * d];
-        q1[d] = pw1[2 * d];
-    }
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) wa[d][ht] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 16 * d);
     __syncthreads();
-    f32x16 c00 = {}, c01 = {}, c10 = {}, c11 = {};   // c<b tile><h tile>
-    const float* xa = s_t + r * F2_LD + 4 * g;
-    const float* xb = s_t + (32 + r) * F2_LD + 4 * g;
+    f32x4 acc[NT][4];
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) acc[ht][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float* xr = s_t + r * F2_LD + 4 * g;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const int d = c % PD;
-        const float4 w0 = q0[d], w1 = q1[d];
+        float4 a[NT];
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) a[ht] = wa[d][ht];
         if (c + PD < NC) {
-            q0[d] = pw0[2 * (c + PD)];
-            q1[d] = pw1[2 * (c + PD)];
+#pragma unroll
+            for (int ht = 0; ht < NT; ++ht)
+                wa[d][ht] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 16 * (c + PD));
         }
         __builtin_amdgcn_sched_barrier(0);   // keep the W2a prefetch ahead of this chunk's MFMAs
-        const float4 a0 = *reinterpret_cast<const float4*>(xa + 8 * c);
-        const float4 a1 = *reinterpret_cast<const float4*>(xb + 8 * c);
-        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, w0.x, c00, 0, 0, 0);
-        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, w0.x, c10, 0, 0, 0);
-        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.x, w1.x, c01, 0, 0, 0);
-        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.x, w1.x, c11, 0, 0, 0);
-        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, w0.y, c00, 0, 0, 0);
-        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, w0.y, c10, 0, 0, 0);
-        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.y, w1.y, c01, 0, 0, 0);
-        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.y, w1.y, c11, 0, 0, 0);
-        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, w0.z, c00, 0, 0, 0);
-        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, w0.z, c10, 0, 0, 0);
-        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.z, w1.z, c01, 0, 0, 0);
-        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.z, w1.z, c11, 0, 0, 0);
-        c00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, w0.w, c00, 0, 0, 0);
-        c10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, w0.w, c10, 0, 0, 0);
-        c01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0.w, w1.w, c01, 0, 0, 0);
-        c11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1.w, w1.w, c11, 0, 0, 0);
+        float4 xb[4];
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) xb[bt] = *reinterpret_cast<const float4*>(xr + 16 * bt * F2_LD + 16 * c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int ht = 0; ht < NT; ++ht)
+#pragma unroll
+                for (int bt = 0; bt < 4; ++bt)
+                    acc[ht][bt] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(a[ht], e), f4c(xb[bt], e), acc[ht][bt], 0, 0, 0);
+    }
+    // relu(hidT + b2a) in place: register q of lane (g, r) in tile (ht, bt) is hidden unit hw0 + 16 ht + 4g + q
+    // of sequence b0 + 16 bt + r
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht) {
+        const float4 bias = *reinterpret_cast<const float4*>(b2a + hw0 + 16 * ht + 4 * g);
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[ht][bt][q] = fmaxf(__fadd_rn(acc[ht][bt][q], f4c(bias, q)), 0.0f);
+    }
+    // outT[j][b] over this wave's hidden units: A = W2b[j][h] (rows j = 16 jt + r), B = hidT from registers
+    const float m0 = r < nout ? 1.0f : 0.0f, m1 = 16 + r < nout ? 1.0f : 0.0f;
+    const float* pb0 = W2b + (size_t)min(r, nout - 1) * dH + hw0 + 4 * g;
+    const float* pb1 = W2b + (size_t)min(16 + r, nout - 1) * dH + hw0 + 4 * g;
+    f32x4 o[2][4];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) o[jt][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht) {
+        float4 u0 = *reinterpret_cast<const float4*>(pb0 + 16 * ht);
+        float4 u1 = *reinterpret_cast<const float4*>(pb1 + 16 * ht);
+        u0.x *= m0; u0.y *= m0; u0.z *= m0; u0.w *= m0;
+        u1.x *= m1; u1.y *= m1; u1.z *= m1; u1.w *= m1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int bt = 0; bt < 4; ++bt) {
+                o[0][bt] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(u0, q), acc[ht][bt][q], o[0][bt], 0, 0, 0);
+                o[1][bt] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4c(u1, q), acc[ht][bt][q], o[1][bt], 0, 0, 0);
+            }
     }
     __syncthreads();   // every wave is done with the x2 tile
-    {
-        // C/D of 32x32: col = lane & 31 (hidden unit), row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5) (b)
-        const int hA = 64 * w + r, hB = hA + 32;
-        const float bA = b2a[h0 + hA], bB = b2a[h0 + hB];
+    // wave partials: register q of o[jt][bt] is outT[16 jt + 4g + q][16 bt + r]
+    float* red = s_t + w * 32 * F2_RS;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            const int row = (q & 3) + 8 * (q >> 2) + 4 * g;
-            s_t[row * F2_LD + hA] = fmaxf(__fadd_rn(c00[q], bA), 0.0f);
-            s_t[(32 + row) * F2_LD + hA] = fmaxf(__fadd_rn(c10[q], bA), 0.0f);
-            s_t[row * F2_LD + hB] = fmaxf(__fadd_rn(c01[q], bB), 0.0f);
-            s_t[(32 + row) * F2_LD + hB] = fmaxf(__fadd_rn(c11[q], bB), 0.0f);
-        }
-    }
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[(16 * jt + 4 * g + q) * F2_RS + 16 * bt + r] = o[jt][bt][q];
     __syncthreads();
-    {
-        // wave w: b rows 16w..16w+15 x outputs 0..31 (two 16x16 tiles), K = the slab's 256 hidden units
-        const int g4 = l >> 4, r4 = l & 15;
-        const float* ph = s_t + (16 * w + r4) * F2_LD + 4 * g4;
-        const int j0 = r4, j1 = 16 + r4;
-        const float4* u0p = reinterpret_cast<const float4*>(W2b + (size_t)min(j0, nout - 1) * dH + h0) + g4;
-        const float4* u1p = reinterpret_cast<const float4*>(W2b + (size_t)min(j1, nout - 1) * dH + h0) + g4;
-        const float m0 = j0 < nout ? 1.0f : 0.0f, m1 = j1 < nout ? 1.0f : 0.0f;
-        f32x4 e0 = {}, e1 = {};
-#pragma unroll 4
-        for (int c = 0; c < F2_HT / 16; ++c) {
-            const float4 hv = *reinterpret_cast<const float4*>(ph + 16 * c);
-            float4 u0 = u0p[4 * c], u1 = u1p[4 * c];
-            u0.x *= m0; u0.y *= m0; u0.z *= m0; u0.w *= m0;
-            u1.x *= m1; u1.y *= m1; u1.z *= m1; u1.w *= m1;
-            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.x, u0.x, e0, 0, 0, 0);
-            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.x, u1.x, e1, 0, 0, 0);
-            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.y, u0.y, e0, 0, 0, 0);
-            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.y, u1.y, e1, 0, 0, 0);
-            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.z, u0.z, e0, 0, 0, 0);
-            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.z, u1.z, e1, 0, 0, 0);
-            e0 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.w, u0.w, e0, 0, 0, 0);
-            e1 = __builtin_amdgcn_mfma_f32_16x16x4f32(hv.w, u1.w, e1, 0, 0, 0);
-        }
-        // C/D of 16x16: col = lane & 15 (output j), row = 4 (lane >> 4) + reg (b)
+    {   // thread t: sequence t >> 2, outputs 8 (t & 3) .. + 7; waves added in order
+        const int bb = t >> 2, j0 = 8 * (t & 3);
+        float v[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int b = b0 + 16 * w + 4 * g4 + q;
-            if (b < B) {
-                float* dst = part + ((size_t)slab * B + b) * 32;
-                dst[r4] = e0[q];
-                dst[16 + r4] = e1[q];
-            }
+        for (int jj = 0; jj < 8; ++jj) {
+            const float* p0 = s_t + (j0 + jj) * F2_RS + bb;
+            v[jj] = __fadd_rn(__fadd_rn(__fadd_rn(p0[0], p0[32 * F2_RS]), p0[64 * F2_RS]), p0[96 * F2_RS]);
+        }
+        if (b0 + bb < B) {
+            float4* dst = reinterpret_cast<float4*>(part + ((size_t)slab * B + b0 + bb) * 32 + j0);
+            dst[0] = make_float4(v[0], v[1], v[2], v[3]);
+            dst[1] = make_float4(v[4], v[5], v[6], v[7]);
         }
     }
 }
@@ -722,7 +737,7 @@ static bool knet_ok(const traj_knet_net* w) {
            w->gru_q_wih && w->gru_q_bih && w->gru_q_whh && w->gru_q_bhh && w->gru_sigma_wih && w->gru_sigma_bih &&
            w->gru_sigma_whh && w->gru_sigma_bhh && w->fc1_w && w->fc1_b && w->fc7_w && w->fc7_b && w->gru_s_wih &&
            w->gru_s_bih && w->gru_s_whh && w->gru_s_bhh && w->fc3_w && w->fc3_b && w->fc4_w && w->fc4_b && w->innov_logit &&
-           w->d_fc2h > 0 && w->d_fc2h % F2_HT == 0 && w->fc2a_w && w->fc2a_b && w->fc2b_w && w->fc2b_b;
+           w->d_fc2h > 0 && w->d_fc2h % 256 == 0 && w->fc2a_w && w->fc2a_b && w->fc2b_w && w->fc2b_b;
 }
 static KNet knet_args(const traj_knet_net* w, const float* packed) {
     const PackPlan pl = pack_plan(w);
@@ -776,7 +791,7 @@ int traj_knet_front_f32(const traj_vehicle_params* p, const traj_knet_limits* li
 
 size_t traj_knet_fc2_workspace_bytes(const traj_knet_net* net, int B) {
     if (!knet_ok(net) || B < 0) return 0;
-    return (size_t)(net->d_fc2h / F2_HT) * (size_t)B * 32 * sizeof(float);
+    return (size_t)(net->d_fc2h / fc2_slab(net->d_fc2h)) * (size_t)B * 32 * sizeof(float);
 }
 
 int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* ws, size_t ws_bytes, void* stream) {
@@ -784,11 +799,15 @@ int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* w
     if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
     if (B == 0) return TRAJ_OK;
     if (!x2 || !ws || ws_bytes < traj_knet_fc2_workspace_bytes(net, B) || ((uintptr_t)x2 & 15) ||
-        ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2b_w & 15))
+        ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2a_b & 15) || ((uintptr_t)net->fc2b_w & 15))
         return TRAJ_E_ARG;
-    const int nslab = net->d_fc2h / F2_HT, nbb = nblk(B, F2_BT);
-    hipLaunchKernelGGL(knet_fc2_kernel, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2,
-                       net->fc2a_w, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
+    const int hs = fc2_slab(net->d_fc2h), nslab = net->d_fc2h / hs, nbb = nblk(B, F2_BT);
+    if (hs == 320)
+        hipLaunchKernelGGL(knet_fc2_kernel<5>, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h,
+                           x2, net->fc2a_w, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
+    else
+        hipLaunchKernelGGL(knet_fc2_kernel<4>, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h,
+                           x2, net->fc2a_w, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
@@ -801,7 +820,7 @@ int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, con
     if (!packed || ((uintptr_t)packed & 15) || !x2 || !ws || !m1x_prior || !dy || !h_sigma || !x_post)
         return TRAJ_E_ARG;
     hipLaunchKernelGGL(knet_back_kernel, dim3(nblk(B, KS)), dim3(KT), 0, (hipStream_t)stream, knet_args(net, packed),
-                       B, x2, ws, net->d_fc2h / F2_HT, m1x_prior, dy, h_sigma, x_post, out, out_stride_b,
+                       B, x2, ws, net->d_fc2h / fc2_slab(net->d_fc2h), m1x_prior, dy, h_sigma, x_post, out, out_stride_b,
                        out_stride_c, KG_out);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
