@@ -25,8 +25,10 @@
  *   - All array pointers are DEVICE pointers (hipMalloc / torch.cuda memory), row-major, float64
  *     (the reference computes in numpy float64).  Shapes are given per argument.
  *   - `stream` is a hipStream_t (NULL = default stream).  Calls are asynchronous; they never
- *     allocate, copy to the host or synchronize, so they can be captured in a hipGraph.  Scratch
- *     memory is the caller's `workspace` (size from traj_mpc_workspace_bytes).
+ *     copy to the host or synchronize, so they can be captured in a hipGraph.  Scratch memory is
+ *     the caller's `workspace` (size from traj_mpc_workspace_bytes); the one exception is the
+ *     state-bound solver (x_lo / x_hi, traj_mpc_step_batch / traj_mpc_qp_batch only), which takes
+ *     its per-call scratch stream-ordered (hipMallocAsync / hipFreeAsync on `stream`).
  *   - Return value: 0 on success, negative TRAJ_E_* on argument / launch errors.
  *   - Per-instance solver outcome is written to `status` (TRAJ_STATUS_*, same numbering as the
  *     CVXPY status strings listed below).  Like mpc_6stati.py:257-262, an instance whose status
@@ -73,7 +75,10 @@ typedef struct {
     double R[4], Rd[4];               /* :132-133, 2x2 row-major; the symmetric part is used */
     double u_lo[2], u_hi[2];          /* u_bounds  :135-136 */
     double du_lo[2], du_hi[2];        /* du_bounds :137-138 */
-    int has_x_lo, has_x_hi;           /* x_lo / x_hi given (:139-140, :208-213) */
+    int has_x_lo, has_x_hi;           /* x_lo / x_hi given (:139-140, :208-213); a side at -inf / inf
+                                       * (|bound| >= 1e30) adds no rows.  With a finite bound the step
+                                       * runs the general condensed-QP solver (dense state rows);
+                                       * the closed-loop entry points return TRAJ_E_UNSUPPORTED */
     double x_lo[6], x_hi[6];
     double eps_abs, eps_rel, eps_prim_inf, rho, sigma, alpha, delta;
     int max_iter, check_interval, scaling_iters, polish, polish_refine_iter, adaptive_rho;

@@ -193,9 +193,11 @@ static void chol_solve(const double* L, int n, double* b) {
         for (int k = 0; k < i; ++k) t -= L[i * n + k] * b[k];
         b[i] = t / L[i * n + i];
     }
+    /* back substitution with each row's terms in descending k: the order in which a column-oriented
+     * (lane-parallel) solve produces them, so the GPU's state-bound solver can keep the same arithmetic */
     for (int i = n - 1; i >= 0; --i) {
         double t = b[i];
-        for (int k = i + 1; k < n; ++k) t -= L[k * n + i] * b[k];
+        for (int k = n - 1; k > i; --k) t -= L[k * n + i] * b[k];
         b[i] = t / L[i * n + i];
     }
 }

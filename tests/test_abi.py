@@ -141,13 +141,17 @@ def test_argument_errors_are_reported_before_any_launch(L):
     fake = C.c_void_p(16)
     args = [fake] * 11
     assert L.traj_mpc_step_batch(C.byref(p), C.byref(c), 4, *args, fake, 8, nul) == _lib.TRAJ_E_ARG
-    # state bounds are not implemented on the HIP path: reported, never silently ignored
+    # state bounds run on the general solver for the step / QP entry points; the closed loop (whose
+    # reference caller never passes them) reports them as unsupported, never silently ignored
     cx = _lib.default_config(20, 0.05)
     cx.has_x_lo = 1
     for i in range(6):
         cx.x_lo[i] = -1e3
-    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cx), 0, *([nul] * 11), nul, 0, nul) == \
-        _lib.TRAJ_E_UNSUPPORTED
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cx), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_OK
+    ps = _lib.Paths()
+    ps.kmax, ps.kind, ps.pc = 0, 16, 16                      # never dereferenced at B = 0
+    assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 0, nul, nul, nul, 0, 0, nul, nul, nul,
+                                   nul, nul, 0, nul) == _lib.TRAJ_E_UNSUPPORTED
 
 
 def test_check_raises():

@@ -11,6 +11,7 @@
 
 #include "../../include/trajmpc.h"
 #include "mpc_common.h"
+#include "mpc_general.h"
 #include "mpc_linearize.h"
 #include "physics.h"
 
@@ -194,18 +195,34 @@ static int launch_mpc(const KArgs& a, hipStream_t st, int mode) {
     return TRAJ_E_ARG;
 }
 
-static int check_cfg(const traj_mpc_config* c) {
+// state bounds (mpc_6stati.py:208-213) with at least one finite side
+static bool state_bounds_active(const traj_mpc_config* c) {
+    for (int i = 0; i < 6; ++i) {
+        if (c->has_x_lo && c->x_lo[i] > -INFTY) return true;
+        if (c->has_x_hi && c->x_hi[i] < INFTY) return true;
+    }
+    return false;
+}
+
+// allow_sb: the caller can run the general (state-bound) solver; the closed-loop entry points cannot
+static int check_cfg(const traj_mpc_config* c, bool allow_sb = false) {
     if (!c) return TRAJ_E_ARG;
     if (c->N < 1 || c->N > TRAJ_MAX_N) return TRAJ_E_ARG;
     if (!(c->Ts > 0.0) || c->max_iter < 1 || c->check_interval < 1 || c->scaling_iters < 0) return TRAJ_E_ARG;
     if (c->polish_mode != 0 && c->polish_mode != 1) return TRAJ_E_ARG;
-    if (c->has_x_lo || c->has_x_hi) {
-        // state bounds (mpc_6stati.py:208-213): accepted only when every bound is infinite
-        for (int i = 0; i < 6; ++i) {
-            if (c->has_x_lo && c->x_lo[i] > -INFTY) return TRAJ_E_UNSUPPORTED;
-            if (c->has_x_hi && c->x_hi[i] < INFTY) return TRAJ_E_UNSUPPORTED;
-        }
-    }
+    if (!allow_sb && state_bounds_active(c)) return TRAJ_E_UNSUPPORTED;
+    return TRAJ_OK;
+}
+
+// the general solver (mpc_general.h) for configurations with state bounds: per-call scratch,
+// allocated and released stream-ordered on the caller's stream
+static int launch_general(const KArgs& a, hipStream_t st) {
+    const size_t per = gen_ws_doubles(a.c.N);
+    void* gws = nullptr;
+    if (hipMallocAsync(&gws, (size_t)a.B * per * sizeof(double), st) != hipSuccess) return TRAJ_E_LAUNCH;
+    hipLaunchKernelGGL(solve_gen_kernel, dim3(a.B), dim3(GEN_NT), 0, st, a, (double*)gws, per);
+    const bool ok = hipGetLastError() == hipSuccess;
+    if (hipFreeAsync(gws, st) != hipSuccess || !ok) return TRAJ_E_LAUNCH;
     return TRAJ_OK;
 }
 
@@ -371,7 +388,7 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
                       double* X_opt, double* U_opt, int* iters, int* polished, void* ws, size_t ws_bytes,
                       void* stream, bool lin) {
     if (!p || B < 0) return TRAJ_E_ARG;
-    int e = check_cfg(c);
+    int e = check_cfg(c, true);
     if (e) return e;
     if (B == 0) return TRAJ_OK;
     if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
@@ -393,6 +410,7 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     a.iters = iters; a.polished = polished;
     a.dbg = g_dbg;
     if (lin) launch_linearize(a, (hipStream_t)stream, false);
+    if (state_bounds_active(c)) return launch_general(a, (hipStream_t)stream);
     return launch_mpc(a, (hipStream_t)stream, lin ? 0 : 1);
 }
 
