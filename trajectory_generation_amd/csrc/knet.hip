@@ -132,12 +132,14 @@ __global__ __launch_bounds__(256) void knet_update_kernel(int B, const float* __
 // A workgroup owns KS sequences through every layer (no cross-workgroup dependency); activations stay
 // in LDS, weights stream from L2 in the packed layout P[k4][j][4] = W[j][4 k4 + c] (zero past K), so
 // the lanes of a wave (consecutive outputs j) read one contiguous 1 KiB run per float4 load.  GRU
-// cells: a thread per hidden unit and half of the sequences forms the six gate dot products and
-// applies torch's GRU gate math (as knet_gru_kernel).  Every dot product is a k-ordered fmaf chain
+// cells: a thread per hidden unit and K quarter forms the six gate dot products over its quarter; the
+// thread (unit, quarter q) then adds the four quarters' partials of sequence q and applies torch's GRU
+// gate math (as knet_gru_kernel).  Every dot product is a k-ordered fmaf chain
 // started at the bias: float32 results within rounding of the library GEMM path.
 constexpr int KS = 4;        // sequences per workgroup
 constexpr int KH = 128;      // hidden size (hidden_dim_gru)
-constexpr int KT = 256;      // threads per workgroup
+constexpr int KQ = 4;        // K parts of every dot product (thread t: unit t & 127, part t >> 7)
+constexpr int KT = KH * KQ;  // threads per workgroup: 8 waves, two per SIMD
 
 struct KNet {
     int m, n, dFC5, dFC1, dFC7, dFC3;
@@ -145,9 +147,9 @@ struct KNet {
     const float4 *W5, *WiQ, *WhQ, *WiG, *WhG, *W1, *W7, *WiS, *WhS, *W3, *W4;   // packed
 };
 
-// packed rows of 4 k per matrix: K rounded up to a multiple of 32 (zero weights past K), so that each
-// half of a split dot product runs a whole number of KD-row prefetch groups
-__host__ __device__ inline int k4_(int K) { return ((K + 31) / 32) * 8; }
+// packed rows of 4 k per matrix: K rounded up to a multiple of 64 (zero weights past K), so that each
+// quarter of a split dot product runs a whole number of KD-row prefetch groups
+__host__ __device__ inline int k4_(int K) { return ((K + 63) / 64) * 16; }
 
 // Packed-buffer offsets (in floats) of the eleven matrices, in the order of traj_knet_net.
 struct PackPlan {
@@ -178,18 +180,20 @@ __global__ void knet_pack_kernel(const float* __restrict__ W, int N, int K, floa
 }
 
 // Activations live in LDS k-major, xT[k][KS] (one float4 = the KS sequences' k-th input), rows
-// zero-padded to a multiple of 4.  Dot products are split over K between the two halves of the
-// workgroup (thread t: output / hidden unit t & 127, K half t >> 7) and the halves' partial sums are
-// added through LDS; weight loads run KD float4 rows ahead of the FMAs (one wave per SIMD here, so
-// the L2 latency must be covered inside the wave).
+// zero-padded to a multiple of 4.  Dot products are split over K between the four quarters of the
+// workgroup (thread t: output / hidden unit t & 127, K quarter t >> 7) and the quarters' partial sums
+// are added through LDS in quarter order; weight loads run KD float4 rows ahead of the FMAs, and the
+// two waves of each SIMD cover each other's L2 latency.
 constexpr int KD = 4;
 
-// acc[g][s] += sum_{k4 in [k4b, k4e)} xT[4 k4 + c][s] * P[k4][j + g * KH][c]  (P rows: NR per k4)
+// acc[g][s] += sum_{k4 in [k4b, k4e)} xT[4 k4 + c][s] * P[k4][j + g * KH][c]  (P rows: NR per k4).
+// Measured on MI355X (front launch, B = 1024): this compact runtime loop 24.7 us; the same loop with
+// compile-time trip counts 27.5 us; fully unrolled straight-line code 29.4 us (register spills); a
+// cross-layer chained prefetch gave nothing -- the chain is bound by per-layer barrier / LDS / load
+// latency, not by one stalled group.
 template <int G>
 __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const float4* __restrict__ P, int NR, int j,
                                        float (&acc)[G][KS]) {
-    // k4e - k4b is a multiple of KD (k4_ padding); loads past the range are clamped, not skipped, so the
-    // loop has no divergent branches around its loads
     float4 wb[KD][G];
 #pragma unroll
     for (int d = 0; d < KD; ++d)
@@ -204,7 +208,7 @@ __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const 
             float4 w[G];
 #pragma unroll
             for (int g = 0; g < G; ++g) w[g] = wb[d][g];
-            const int kn = min(kk + KD, k4e - 1);
+            const int kn = min(kk + KD, k4e - 1);   // past the range: a harmless reload of the last row
 #pragma unroll
             for (int g = 0; g < G; ++g) wb[d][g] = P[(size_t)kn * NR + j + g * KH];
 #pragma unroll
@@ -218,23 +222,30 @@ __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const 
     }
 }
 
+constexpr int K4_H = KH / 4;   // rows of 4 of every W_hh
+
 // Dense layer: outT[j][s] = act(b[j] + sum_k xT[k][s] W[j][k]) for j < N <= KH (outT: LDS, k-major).
-// xch: LDS scratch of KH * KS floats.  Called by every thread of the workgroup.
+// xch: LDS scratch of (KQ - 1) * KH * KS floats.  Called by every thread of the workgroup.
 __device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* __restrict__ P,
                                          const float* __restrict__ bias, int N, float* outT, bool relu, float* xch,
                                          int t) {
-    const int j = t & (KH - 1), half = t >> 7, h2 = K4 >> 1;
+    const int j = t & (KH - 1), part = t >> 7, h4 = K4 / KQ;
     float acc[1][KS] = {{0.0f, 0.0f, 0.0f, 0.0f}};
     if (j < N) {
-        if (half == 0) acc[0][0] = acc[0][1] = acc[0][2] = acc[0][3] = bias[j];
-        dot_ks<1>(xT, half * h2, (half + 1) * h2, P, N, j, acc);
-        if (half) *reinterpret_cast<float4*>(xch + KS * j) = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+        if (part == 0) acc[0][0] = acc[0][1] = acc[0][2] = acc[0][3] = bias[j];
+        dot_ks<1>(xT, part * h4, (part + 1) * h4, P, N, j, acc);
+        if (part)
+            *reinterpret_cast<float4*>(xch + ((part - 1) * KH + j) * KS) =
+                make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
     }
     __syncthreads();
-    if (j < N && half == 0) {
-        const float4 o = *reinterpret_cast<const float4*>(xch + KS * j);
-        float4 r = make_float4(__fadd_rn(acc[0][0], o.x), __fadd_rn(acc[0][1], o.y), __fadd_rn(acc[0][2], o.z),
-                               __fadd_rn(acc[0][3], o.w));
+    if (j < N && part == 0) {
+        float4 r = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+#pragma unroll
+        for (int q = 1; q < KQ; ++q) {
+            const float4 o = *reinterpret_cast<const float4*>(xch + ((q - 1) * KH + j) * KS);
+            r = make_float4(__fadd_rn(r.x, o.x), __fadd_rn(r.y, o.y), __fadd_rn(r.z, o.z), __fadd_rn(r.w, o.w));
+        }
         if (relu) r = make_float4(fmaxf(r.x, 0.0f), fmaxf(r.y, 0.0f), fmaxf(r.z, 0.0f), fmaxf(r.w, 0.0f));
         *reinterpret_cast<float4*>(outT + KS * j) = r;
     }
@@ -242,50 +253,51 @@ __device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* 
 }
 
 // GRU cell (torch.nn.GRU, one layer, one step) for the KS sequences: xT [K][KS], hT [KH][KS] -> houtT.
-// Half 0 finishes sequences 0, 1 and half 1 sequences 2, 3.  xch: LDS scratch of 2 * KH * 12 floats.
+// Thread (unit u, quarter q) forms its quarter's partial gates for all KS sequences, then finishes
+// sequence q from the four quarters' partials (added in quarter order).  xch: LDS scratch of
+// KQ * KH * 6 * KS floats.
 __device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT, const float4* __restrict__ Wi,
                                        const float* __restrict__ bi, const float4* __restrict__ Wh,
                                        const float* __restrict__ bh, float* houtT, float* xch, int t) {
-    const int u = t & (KH - 1), half = t >> 7;
+    static_assert(KQ == KS, "one finished sequence per K quarter");
+    const int u = t & (KH - 1), part = t >> 7;
     float gi[3][KS], gh[3][KS];
 #pragma unroll
     for (int g = 0; g < 3; ++g)
 #pragma unroll
         for (int q = 0; q < KS; ++q) {
-            gi[g][q] = half ? 0.0f : bi[g * KH + u];
-            gh[g][q] = half ? 0.0f : bh[g * KH + u];
+            gi[g][q] = part ? 0.0f : bi[g * KH + u];
+            gh[g][q] = part ? 0.0f : bh[g * KH + u];
         }
-    const int hi = K4 >> 1;
-    dot_ks<3>(xT, half * hi, (half + 1) * hi, Wi, 3 * KH, u, gi);
-    dot_ks<3>(hT, half * (KH / 8), (half + 1) * (KH / 8), Wh, 3 * KH, u, gh);
-    // hand the other half its two sequences' partial sums
-    float* mine = xch + (size_t)(half * KH + u) * 12;
-    const int so = half ? 0 : 2;   // the sequences the other half finishes
+    const int hi = K4 / KQ, hh = K4_H / KQ;
+    dot_ks<3>(xT, part * hi, (part + 1) * hi, Wi, 3 * KH, u, gi);
+    dot_ks<3>(hT, part * hh, (part + 1) * hh, Wh, 3 * KH, u, gh);
+    // publish: xch[part][u][sequence][gi r z n | gh r z n]
+    float* mine = xch + (size_t)(part * KH + u) * 6 * KS;
 #pragma unroll
-    for (int g = 0; g < 3; ++g) {
-        mine[4 * g + 0] = gi[g][so];
-        mine[4 * g + 1] = gi[g][so + 1];
-        mine[4 * g + 2] = gh[g][so];
-        mine[4 * g + 3] = gh[g][so + 1];
+    for (int q = 0; q < KS; ++q) {
+        *reinterpret_cast<float2*>(mine + 6 * q) = make_float2(gi[0][q], gi[1][q]);
+        *reinterpret_cast<float2*>(mine + 6 * q + 2) = make_float2(gi[2][q], gh[0][q]);
+        *reinterpret_cast<float2*>(mine + 6 * q + 4) = make_float2(gh[1][q], gh[2][q]);
     }
     __syncthreads();
-    const float* other = xch + (size_t)((1 - half) * KH + u) * 12;
-    const int s0 = half ? 2 : 0;
+    const int sq = part;   // the sequence this thread finishes
+    float ir[3] = {0.0f, 0.0f, 0.0f}, hr[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        float ir[3], hr[3];
+    for (int q = 0; q < KQ; ++q) {
+        const float* o = xch + (size_t)(q * KH + u) * 6 * KS + 6 * sq;
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
-            ir[g] = __fadd_rn(gi[g][s0 + q], other[4 * g + q]);
-            hr[g] = __fadd_rn(gh[g][s0 + q], other[4 * g + 2 + q]);
+            ir[g] = q ? __fadd_rn(ir[g], o[g]) : o[g];
+            hr[g] = q ? __fadd_rn(hr[g], o[3 + g]) : o[3 + g];
         }
-        // ATen GRUCell: r = sigmoid(h_r + i_r), z = sigmoid(h_z + i_z), n = tanh(i_n + h_n * r), h' = (h - n) z + n
-        const float r = sigmoidf_(__fadd_rn(hr[0], ir[0]));
-        const float z = sigmoidf_(__fadd_rn(hr[1], ir[1]));
-        const float nn = tanhf(__fadd_rn(ir[2], __fmul_rn(hr[2], r)));
-        const float hv = hT[u * KS + s0 + q];
-        houtT[u * KS + s0 + q] = __fadd_rn(__fmul_rn(__fsub_rn(hv, nn), z), nn);
     }
+    // ATen GRUCell: r = sigmoid(h_r + i_r), z = sigmoid(h_z + i_z), n = tanh(i_n + h_n * r), h' = (h - n) z + n
+    const float r = sigmoidf_(__fadd_rn(hr[0], ir[0]));
+    const float z = sigmoidf_(__fadd_rn(hr[1], ir[1]));
+    const float nn = tanhf(__fadd_rn(ir[2], __fmul_rn(hr[2], r)));
+    const float hv = hT[u * KS + sq];
+    houtT[u * KS + sq] = __fadd_rn(__fmul_rn(__fsub_rn(hv, nn), z), nn);
     __syncthreads();
 }
 
@@ -301,11 +313,11 @@ __global__ __launch_bounds__(KT) void knet_front_kernel(KP p, traj_knet_limits L
     __shared__ __attribute__((aligned(16))) float s_q[KH * KS];      // new h_Q
     __shared__ __attribute__((aligned(16))) float s_g[KH * KS];      // out_Sigma
     __shared__ __attribute__((aligned(16))) float s_hs[KH * KS];     // new h_S
-    __shared__ __attribute__((aligned(16))) float s_pr[32 * KS];     // prior, zero-padded
-    __shared__ __attribute__((aligned(16))) float s_dy[32 * KS];     // innovation, zero-padded
-    __shared__ __attribute__((aligned(16))) float s_o5[32 * KS];     // FC5 output, zero-padded
-    __shared__ __attribute__((aligned(16))) float s_c1[32 * KS];     // [FC1 | FC7], zero-padded
-    __shared__ __attribute__((aligned(16))) float s_x[2 * KH * 12];  // half-sum exchange
+    __shared__ __attribute__((aligned(16))) float s_pr[64 * KS];     // prior, zero-padded to k4_
+    __shared__ __attribute__((aligned(16))) float s_dy[64 * KS];     // innovation, zero-padded
+    __shared__ __attribute__((aligned(16))) float s_o5[64 * KS];     // FC5 output, zero-padded
+    __shared__ __attribute__((aligned(16))) float s_c1[64 * KS];     // [FC1 | FC7], zero-padded
+    __shared__ __attribute__((aligned(16))) float s_x[KQ * KH * 6 * KS];   // K-quarter partial sums
     const int t = threadIdx.x, b0 = blockIdx.x * KS;
     const int nb = min(KS, B - b0);
     for (int i = t; i < 3 * KS * KH; i += KT) {   // coalesced row reads -> k-major LDS
@@ -313,7 +325,7 @@ __global__ __launch_bounds__(KT) void knet_front_kernel(KP p, traj_knet_limits L
         const float* src = (w == 0) ? hQ : (w == 1 ? hSig : hS);
         s_h[w][k * KS + s] = (s < nb) ? src[(size_t)(b0 + s) * KH + k] : 0.0f;
     }
-    if (t < 32 * KS) s_o5[t] = s_c1[t] = s_pr[t] = s_dy[t] = 0.0f;
+    if (t < 64 * KS) s_o5[t] = s_c1[t] = s_pr[t] = s_dy[t] = 0.0f;
     __syncthreads();
     if (t < KS) {
         float pr[6] = {0, 0, 0, 0, 0, 0}, e[5] = {0, 0, 0, 0, 0};
@@ -500,11 +512,11 @@ __global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const fl
                                                        const float* __restrict__ prior, const float* __restrict__ dy,
                                                        float* hSig, float* x_post, float* out, int o_sb, int o_sc,
                                                        float* KG_out) {
-    __shared__ __attribute__((aligned(16))) float s_a[(KH + 32) * KS];    // [h_S | KG | 0]: FC3's input
+    __shared__ __attribute__((aligned(16))) float s_a[(KH + 64) * KS];    // [h_S | KG | 0]: FC3's input
     __shared__ __attribute__((aligned(16))) float s_b[(KH + 64) * KS];    // [out_Sigma | FC3 | 0]: FC4's input
     __shared__ __attribute__((aligned(16))) float s_o[KH * KS];           // FC4 output (new h_Sigma)
-    __shared__ __attribute__((aligned(16))) float s_x[2 * KH * 12];
-    __shared__ float s_red[KS][32][2];
+    __shared__ __attribute__((aligned(16))) float s_x[(KQ - 1) * KH * KS];   // K-quarter partial sums
+    __shared__ float s_red[KS][32][4];
     const int t = threadIdx.x, b0 = blockIdx.x * KS;
     const int nb = min(KS, B - b0);
     const int nm = net.n * net.m;
@@ -515,13 +527,14 @@ __global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const fl
         else s_a[(k - KH) * KS + s] = v;
     }
     for (int i = t; i < 64 * KS; i += KT) s_b[KH * KS + i] = 0.0f;
-    {   // KG = b2b + sum over FC2's slabs: thread (s, j, parity) sums the even or odd slabs
-        const int s = t >> 6, j = (t >> 1) & 31, q = t & 1;
+    for (int i = t; i < 32 * KS; i += KT) s_a[(KH + 32) * KS + i] = 0.0f;
+    {   // KG = b2b + sum over FC2's slabs: thread (s, j, q) sums the slabs sl = q mod 4
+        const int s = t >> 7, j = (t >> 2) & 31, q = t & 3;
         float a = 0.0f;
         if (s < nb) {
             const float* pp = part + ((size_t)b0 + s) * 32 + j;
-#pragma unroll 10
-            for (int sl = q; sl < nslab; sl += 2) a = __fadd_rn(a, pp[(size_t)sl * B * 32]);
+#pragma unroll 8
+            for (int sl = q; sl < nslab; sl += 4) a = __fadd_rn(a, pp[(size_t)sl * B * 32]);
         }
         s_red[s][j][q] = a;
     }
@@ -530,7 +543,8 @@ __global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const fl
         const int s = t >> 5, j = t & 31;
         float v = 0.0f;
         if (j < nm && s < nb) {
-            v = __fadd_rn(net.b2b[j], __fadd_rn(s_red[s][j][0], s_red[s][j][1]));
+            v = __fadd_rn(net.b2b[j], __fadd_rn(__fadd_rn(s_red[s][j][0], s_red[s][j][1]),
+                                                __fadd_rn(s_red[s][j][2], s_red[s][j][3])));
             if (KG_out) KG_out[(size_t)(b0 + s) * nm + j] = v;
         }
         s_a[(KH + j) * KS + s] = v;
