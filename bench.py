@@ -83,9 +83,18 @@ KNET_LIMITS = {"x_min": -5.0, "x_max": 40.0, "y_min": -6.0, "y_max": 6.0, "phi_m
                "vx_min": 0.0, "vx_max": 3.0, "vy_min": -1.0, "vy_max": 1.0, "omega_min": -6.0, "omega_max": 6.0}
 
 
-def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50):
+def knet_fc2_flop(B, model):
+    """Algorithmic FLOP of one knet_fc2_kernel launch: FC2 = Linear(2H, dH) -> ReLU -> Linear(dH, n m)."""
+    H, dH, nm = model.d_hidden_Q, model.d_hidden_FC2, model.n * model.m
+    return 2 * B * (2 * H * dH + dH * nm)
+
+
+def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
+                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r01.json")):
     """Sequences/s of KalmanNet inference (random-init weights of the reference architecture,
-    synthetic normalized inputs resident on the GPU), one step replayed as a HIP graph."""
+    synthetic normalized inputs resident on the GPU), all T fused steps replayed as one HIP graph.
+    The roofline object is the dominant kernel's (knet_fc2_kernel, f32 MFMA), timed with events over
+    standalone launches on the same data."""
     from trajectory_generation_amd import knet as K
     torch.manual_seed(0)
     sysm = K.VehicleModel(0.01, T, T, torch.zeros(6, 1))
@@ -108,7 +117,33 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50):
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
-    dt = timed(fused=True)               # the throughput path: 4 launches per step, T steps in one graph
+    dt = timed(fused=True)               # the throughput path: 3 launches per step, T steps in one graph
+    # the dominant kernel alone (same weights, x2 and workspace as the run): HIP events on the stream
+    S, L = run.fs, _lib.lib()
+    reps = 50
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fc2 = lambda: _lib.check(L.traj_knet_fc2_f32(ctypes.byref(S["net"]), B, ctypes.c_void_p(S["x2"].data_ptr()),  # noqa
+                                                 ctypes.c_void_p(S["ws"][0].data_ptr()), S["ws"][0].numel() * 4,
+                                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                             "traj_knet_fc2_f32")
+    fc2()
+    e0.record()
+    for _ in range(reps):
+        fc2()
+    e1.record()
+    torch.cuda.synchronize()
+    fc2_ms = e0.elapsed_time(e1) / reps
+    fc2_flop = knet_fc2_flop(B, model)
+    fc2_tfs = fc2_flop / (fc2_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(traffic_json):
+        try:
+            with open(traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("batch") == B:
+                traffic = tj.get("hbm_bytes_per_launch", {}).get("knet_fc2_kernel")
+        except (OSError, ValueError):
+            traffic = None
     dt_step_graph = timed(fused=False)   # module-level step (per-layer launches), one-step graph
     achieved = KNET_FLOP_PER_SEQ_STEP * B * T / dt / 1e12
     out = {"metric": f"KalmanNet seq/s (B={B}, T={T})", "value": B / dt, "unit": "sequences/s",
@@ -116,9 +151,13 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50):
            "module_step_graph_value": B / dt_step_graph,
            "config": {"workload": "KalmanNetNN inference (in_mult 5, out_mult 40, hidden 128), random-init weights, "
                                   "synthetic normalized inputs", "batch": B, "T": T, "Ts": 0.01},
-           "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": achieved / FP32_MFMA_PEAK_TFS, "traffic": None,
-                        "flop_per_seq_step": KNET_FLOP_PER_SEQ_STEP}}
+           "roofline": {"bound": "mfma", "achieved": fc2_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": fc2_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
+                        "kernel": "knet_fc2_kernel<5> (FC2: Linear 256->10240, ReLU, Linear 10240->30)",
+                        "kernel_ms": fc2_ms, "flop_per_launch": fc2_flop,
+                        "traffic_source": os.path.relpath(traffic_json, HERE) if traffic is not None else None,
+                        "whole_step": {"achieved": achieved, "frac": achieved / FP32_MFMA_PEAK_TFS,
+                                       "flop_per_seq_step": KNET_FLOP_PER_SEQ_STEP}}}
     if cpu:
         import oracle.knet_oracle as KO  # test infrastructure: CPU-baseline leg only
         w = {k: v.detach().cpu() for k, v in model.state_dict().items()}
@@ -155,6 +194,8 @@ def main():
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
+    ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r01.json"),
+                    help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -280,7 +321,7 @@ def main():
     else:
         out["cpu_baseline"] = None
     if not args.no_knet and world == 1:
-        out["knet"] = knet_measure(dev, cpu=not args.no_cpu)
+        out["knet"] = knet_measure(dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json)
     print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
