@@ -283,15 +283,18 @@ def test_closed_loop_main_py_case_vs_oracle(gpu, oracle_lib):
     assert err[:10].max() <= 1e-7 and err.max() <= 1e-4, err
 
 
-@pytest.mark.parametrize("warm", [0, 1])
-def test_closed_loop_per_step_parity_ts005(gpu, oracle_lib, warm):
+@pytest.mark.parametrize("kind,N,T,B,warm", [("spline", 20, 20, 48, 0), ("spline", 20, 20, 48, 1),
+                                             ("mixed", 40, 30, 32, 0)])
+def test_closed_loop_per_step_parity_ts005(gpu, oracle_lib, kind, N, T, B, warm):
     """SURVEY.md 8(d) gate (1) at Ts = 0.05, where the plant is unstable (rho(A) up to 6.45) and
     1e-12 differences grow ~50x per step: every step of the GPU closed loop is re-solved by the
-    oracle from the GPU's own state and must agree (statuses identical; u_cmd as in the step tests)."""
-    N, Ts, T, B = 20, 0.05, 20, 48
-    w, paths, cfg, res, _ = _closed_loop_both(oracle_lib, "spline", N, Ts, T, warm, B)
+    oracle from the GPU's own state and must agree (statuses identical; u_cmd as in the step tests).
+    The N = 40 case (BASELINE.json configs[2]) drives some instances into solver errors (the
+    40-stage condensed problem of an unstable plant overflows); the oracle reports the same."""
+    Ts = 0.05
+    w, paths, cfg, res, _ = _closed_loop_both(oracle_lib, kind, N, Ts, T, warm, B)
     vr = np.tile(w["vref"], (B, 1))
-    n_same_pol = n = 0
+    n_same_pol = n = n_it = 0
     for t in range(T):
         xt = res["X"][:, t]
         ut = res["U"][:, t - 1] if t > 0 else w["u0"]
@@ -305,10 +308,22 @@ def test_closed_loop_per_step_parity_ts005(gpu, oracle_lib, warm):
         assert np.array_equal(g["status"], ro["status"])
         same = (g["polished"] > 0) == (ro["polished"] > 0)
         du = np.abs(g["u_cmd"] - ro["u_cmd"]).max(axis=1)
-        assert du[same].max() <= 1e-4
+        if N == 20:
+            assert du[same].max() <= 1e-4
+        else:
+            # 40-stage problems of the unstable plant reach condition numbers ~1e9:
+            # polished optima agree to 1e-6; unpolished eps = 1e-5 ADMM points to 1e-3 when both stop at
+            # the same iteration (measured <= 1.6e-4); a different stopping iteration is a different point
+            both = (g["polished"] > 0) & (ro["polished"] > 0)
+            assert du[both].max(initial=0.0) <= 1e-6
+            eq = same & ~both & (g["iters"] == ro["iters"])
+            assert du[eq].max(initial=0.0) <= 1e-3
+            n_it += int((g["iters"] == ro["iters"]).sum())
         n_same_pol += same.sum()
         n += B
     assert n_same_pol / n >= 0.98
+    if N != 20:
+        assert n_it / n >= 0.95
 
 
 def test_closed_loop_history_matches_single_steps(gpu):
