@@ -17,6 +17,11 @@ GRU cells + FC1/FC7 for four sequences per workgroup), ``traj_knet_fc2_f32`` (FC
 cores, its [B, 10240] hidden activation kept on chip), ``traj_knet_back_f32`` (FC3 + FC4 + posterior
 update) -- and captures all T steps in one graph.
 There is no CPU path: the ops raise without the HIP library or a GPU.
+
+Training (``knet_train.py``): with autograd on, the three HIP ops run inside
+``torch.autograd.Function`` s whose backward re-evaluates the same step in torch ops on the device
+and differentiates it -- the expressions of vehicle_model.py / kalman_net.py that the reference's
+autograd differentiates (clamp, max and atan2 subgradients included); the GEMMs are torch's.
 """
 from __future__ import annotations
 
@@ -72,15 +77,127 @@ def knet_prior(params: dict, Ts: float, x_post, u, x_mean, x_std, y_mean, y_std,
     return prior, m1y, dy
 
 
+def _gru_gates(gi, gh, h):
+    out = torch.empty_like(h)
+    B, H = h.shape
+    gi, gh, h = gi.contiguous(), gh.contiguous(), h.contiguous()
+    _lib.check(_lib.lib().traj_knet_gru_gates_f32(B, H, _p(gi), _p(gh), _p(h), _p(out), _stream()),
+               "traj_knet_gru_gates_f32")
+    return out
+
+
 def gru_cell(x, h, gru: nn.GRU):
     """One step of a 1-layer torch.nn.GRU: two GEMMs + the fused gate kernel. x [B,in], h [B,H]."""
     gi = torch.addmm(gru.bias_ih_l0, x, gru.weight_ih_l0.t())
     gh = torch.addmm(gru.bias_hh_l0, h, gru.weight_hh_l0.t())
-    out = torch.empty_like(h)
-    B, H = h.shape
-    _lib.check(_lib.lib().traj_knet_gru_gates_f32(B, H, _p(gi), _p(gh), _p(h), _p(out), _stream()),
-               "traj_knet_gru_gates_f32")
-    return out
+    if torch.is_grad_enabled() and (gi.requires_grad or gh.requires_grad or h.requires_grad):
+        return _GruGatesFn.apply(gi, gh, h)
+    return _gru_gates(gi, gh, h)
+
+
+# ---------------------------------------------------------------- autograd (training, f4)
+
+def torch_prior(params: dict, Ts: float, x_post, u, y, x_mean, x_std, y_mean, y_std, u_mean=None, u_std=None):
+    """kalman_net.py:145-162 with vehicle_model.py:19-153 in torch ops on [B,6] / [B,2] / [B,5] tensors:
+    the expressions whose autograd the reference runs, evaluated by knet_prior's backward."""
+    p = params
+    xs, xm = x_std.reshape(1, 6), x_mean.reshape(1, 6)
+    x = x_post * xs + xm                                                   # _denorm_x
+    uu = u if (u_mean is None or u_std is None) else u * u_std.reshape(1, 2) + u_mean.reshape(1, 2)
+    phi = torch.clamp(x[:, 2], p["phi_min"], p["phi_max"])                # pt_f_cont (:45-79)
+    vx = torch.clamp(x[:, 3], p["vx_min"], p["vx_max"])
+    vy = torch.clamp(x[:, 4], p["vy_min"], p["vy_max"])
+    omega = torch.clamp(x[:, 5], p["omega_min"], p["omega_max"])
+    d, delta = uu[:, 0], uu[:, 1]
+    vx_eff = torch.max(torch.abs(vx), torch.tensor(p["vx_zero"], device=vx.device))   # pt_tire_forces (:19-42)
+    alpha_f = -torch.atan2(omega * p["lf"] + vy, vx_eff) + delta
+    alpha_r = torch.atan2(omega * p["lr"] - vy, vx_eff)
+    alpha_f = torch.clamp(alpha_f, -p["maxAlpha"], p["maxAlpha"])
+    Fy_f = p["Df"] * torch.sin(p["Cf"] * torch.atan(p["Bf"] * alpha_f))
+    Fy_r = p["Dr"] * torch.sin(p["Cr"] * torch.atan(p["Br"] * alpha_r))
+    Frx = (p["Cm1"] - p["Cm2"] * vx_eff) * d - p["Cr0"] - p["Cr2"] * (vx_eff ** 2)
+    m, Iz, lf, lr = p["m"], p["Iz"], p["lf"], p["lr"]
+    xdot = torch.stack([vx * torch.cos(phi) - vy * torch.sin(phi), vx * torch.sin(phi) + vy * torch.cos(phi), omega,
+                        (Frx - Fy_f * torch.sin(delta) + m * vy * omega) / m,
+                        (Fy_r + Fy_f * torch.cos(delta) - m * vx * omega) / m,
+                        (Fy_f * lf * torch.cos(delta) - Fy_r * lr) / Iz], dim=1)
+    xn = x + Ts * xdot                                                      # f (:109-134)
+    lim = [("x_min", "x_max"), ("y_min", "y_max"), ("phi_min", "phi_max"), ("vx_min", "vx_max"),
+           ("vy_min", "vy_max"), ("omega_min", "omega_max")]
+    xn = torch.stack([torch.clamp(xn[:, i], p[a], p[b]) for i, (a, b) in enumerate(lim)], dim=1)
+    prior = (xn - xm) / xs                                                  # _renorm_x
+    m1y = (xn[:, [0, 1, 3, 4, 5]] - y_mean.reshape(1, 5)) / y_std.reshape(1, 5)   # h, _renorm_y
+    return prior, m1y, y - m1y
+
+
+class _KnetPriorFn(torch.autograd.Function):
+    """knet_prior (HIP) forward; backward through torch_prior w.r.t. x_post."""
+
+    @staticmethod
+    def forward(ctx, x_post, u, y, params, Ts, norm):
+        prior, m1y, dy = knet_prior(params, Ts, x_post, u, *norm[:4], y=y, u_mean=norm[4], u_std=norm[5])
+        ctx.save_for_backward(x_post, u, y)
+        ctx.params, ctx.Ts, ctx.norm = params, Ts, norm
+        return prior, m1y, dy
+
+    @staticmethod
+    def backward(ctx, g_prior, g_m1y, g_dy):
+        x_post, u, y = ctx.saved_tensors
+        with torch.enable_grad():
+            xp = x_post.detach().reshape(-1, 6).requires_grad_(True)
+            outs = torch_prior(ctx.params, ctx.Ts, xp, u.reshape(-1, 2), y.reshape(-1, 5), *ctx.norm)
+            pairs = [(o, g) for o, g in zip(outs, (g_prior, g_m1y, g_dy)) if g is not None]
+            gx, = torch.autograd.grad([o for o, _ in pairs], [xp], [g for _, g in pairs])
+        return gx.reshape(x_post.shape), None, None, None, None, None
+
+
+def torch_gru_gates(gi, gh, h):
+    """torch.nn.GRU's gate arithmetic (r, z, n order) on the two GEMM outputs."""
+    H = h.shape[1]
+    r = torch.sigmoid(gi[:, :H] + gh[:, :H])
+    z = torch.sigmoid(gi[:, H:2 * H] + gh[:, H:2 * H])
+    n = torch.tanh(gi[:, 2 * H:] + r * gh[:, 2 * H:])
+    return (1.0 - z) * n + z * h
+
+
+class _GruGatesFn(torch.autograd.Function):
+    """traj_knet_gru_gates_f32 forward; backward through torch_gru_gates."""
+
+    @staticmethod
+    def forward(ctx, gi, gh, h):
+        ctx.save_for_backward(gi, gh, h)
+        return _gru_gates(gi, gh, h)
+
+    @staticmethod
+    def backward(ctx, g):
+        gi, gh, h = ctx.saved_tensors
+        with torch.enable_grad():
+            a, b, c = (t.detach().requires_grad_(True) for t in (gi, gh, h))
+            return torch.autograd.grad(torch_gru_gates(a, b, c), [a, b, c], [g])
+
+
+class _UpdateFn(torch.autograd.Function):
+    """traj_knet_update_f32 forward: x_post = x_prior + sigmoid(innov_logit) KG dy (kalman_net.py:169-178)."""
+
+    @staticmethod
+    def forward(ctx, prior, KG, dy, logit):
+        B, m = prior.shape
+        post = torch.empty((B, m), dtype=torch.float32, device=prior.device)
+        prior_c, KG_c, dy_c, lg = prior.contiguous(), KG.contiguous(), dy.contiguous(), logit.detach().contiguous()
+        _lib.check(_lib.lib().traj_knet_update_f32(B, _p(prior_c), _p(KG_c), _p(dy_c), _p(lg), _p(post), _stream()),
+                   "traj_knet_update_f32")
+        ctx.save_for_backward(prior, KG, dy, logit)
+        return post
+
+    @staticmethod
+    def backward(ctx, g):
+        prior, KG, dy, logit = ctx.saved_tensors
+        with torch.enable_grad():
+            ts = [t.detach().requires_grad_(True) for t in (prior, KG, dy, logit)]
+            B, m = prior.shape
+            n = dy.shape[1]
+            post = ts[0] + (torch.sigmoid(ts[3]) * torch.bmm(ts[1].reshape(B, m, n), ts[2].reshape(B, n, 1))).reshape(B, m)
+            return torch.autograd.grad(post, ts, [g])
 
 
 def _linear(x, lin: nn.Linear, relu: bool):
@@ -208,8 +325,14 @@ class KalmanNetNN(nn.Module):
     # ---------- one step ----------
     def step_prior(self, u, y=None):
         xm, xs, ym, ys = self._norm_tensors()
-        prior, m1y, dy = knet_prior(self.sys.Params, self.sys.Ts, self.m1x_posterior, u, xm, xs, ym, ys, y=y,
-                                    u_mean=self.u_mean, u_std=self.u_std)
+        if y is not None and torch.is_grad_enabled() and self.m1x_posterior.requires_grad:
+            B = self.m1x_posterior.shape[0]
+            prior, m1y, dy = _KnetPriorFn.apply(self.m1x_posterior.reshape(B, 6), u.reshape(B, 2).contiguous(),
+                                                y.reshape(B, 5).contiguous(), self.sys.Params, self.sys.Ts,
+                                                (xm, xs, ym, ys, self.u_mean, self.u_std))
+        else:
+            prior, m1y, dy = knet_prior(self.sys.Params, self.sys.Ts, self.m1x_posterior, u, xm, xs, ym, ys, y=y,
+                                        u_mean=self.u_mean, u_std=self.u_std)
         self.m1x_prior = prior.unsqueeze(2)
         self.m1y = m1y.unsqueeze(2)
         return dy
@@ -240,10 +363,14 @@ class KalmanNetNN(nn.Module):
         dy = self.step_prior(u, y=y)
         KG = self.KGain_step(dy, self.m1x_prior.reshape(B, self.m))
         self.KGain = KG.reshape(self.batch_size, self.m, self.n)
-        post = torch.empty((B, self.m), dtype=torch.float32, device=self.device)
-        prior, KGc = self.m1x_prior.reshape(B, self.m).contiguous(), KG.contiguous()
-        _lib.check(_lib.lib().traj_knet_update_f32(B, _p(prior), _p(KGc), _p(dy), _p(self.innov_logit.detach()),
-                                                   _p(post), _stream()), "traj_knet_update_f32")
+        prior = self.m1x_prior.reshape(B, self.m)
+        if torch.is_grad_enabled() and (prior.requires_grad or KG.requires_grad or self.innov_logit.requires_grad):
+            post = _UpdateFn.apply(prior, KG, dy, self.innov_logit)
+        else:
+            post = torch.empty((B, self.m), dtype=torch.float32, device=self.device)
+            prior, KGc = prior.contiguous(), KG.contiguous()
+            _lib.check(_lib.lib().traj_knet_update_f32(B, _p(prior), _p(KGc), _p(dy), _p(self.innov_logit.detach()),
+                                                       _p(post), _stream()), "traj_knet_update_f32")
         self.m1x_posterior = post.unsqueeze(2)
         return self.m1x_posterior
 
