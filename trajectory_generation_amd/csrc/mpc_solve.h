@@ -21,6 +21,19 @@
 
 namespace tgmpc {
 
+// Fused closed loop: an instance's state (x, u_prev, warm record) passes between workgroups -- on any XCD
+// -- without agent-scope release/acquire fences.  A release at agent scope writes back the whole XCD L2
+// (buffer_wbl2), which at one hand-off per work item flushed the solve's spill lines to HBM (10.4 GB per
+// 200-step launch).  Instead (MI355X_MICROARCH.md, cross-workgroup publish): the state is stored with
+// coherent (sc1) stores, the storing lane waits for them (vmcnt(0)), then stores the step counter sc1;
+// the consumer polls the counter with sc1 loads and reads the state with sc1 loads.
+__device__ __forceinline__ void st_coh(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coh(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // =====================================================================================
 // NN = capacity in QP variables (>= 2N); CLOSED = closed-loop step (window from the state, plant
 // update, history).  A_k, B_k, g_k are read from a.Ad / a.Bd / a.gd ([B,N,36], [B,N,12], [B,N,6]).
@@ -78,7 +91,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         b = a.perm ? a.perm[rank] : rank;
         if (threadIdx.x == 0 && step > 0) {
             int spins = 0;
-            while (__hip_atomic_load(&a.queue[2 + b], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < step) {
+            while (__hip_atomic_load(&a.queue[2 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < step) {
                 __builtin_amdgcn_s_sleep(2);
                 if (++spins > (1 << 22)) {   // bounded: a lost hand-off is reported, never a hang
                     __hip_atomic_store(&a.queue[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -175,7 +188,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // register loops over the full capacity NN rely on
     for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
     for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
-    if (CLOSED) {
+    if (FUSED) {   // the state the instance's previous step published (sc1, see st_coh)
+        if (t < 6) s_x0[t] = ld_coh(a.x_state + 6 * b + t);
+        if (t < 2) s_up[t] = ld_coh(a.u_state + 2 * b + t);
+    } else if (CLOSED) {
         if (t < 6) s_x0[t] = a.x_state[6 * b + t];
         if (t < 2) s_up[t] = a.u_state[2 * b + t];
     } else {
@@ -622,7 +638,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         if (CLOSED && c.warm_start && tstep > 0) {
             if (a.wsWarm) {
                 const double* wv = a.wsWarm + 4 * (size_t)b;
-                if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
+                const double w0 = FUSED ? ld_coh(wv) : wv[0], w1 = FUSED ? ld_coh(wv + 1) : wv[1];
+                if (w1 != 0.0) rho = fmin(fmax(w0, RHO_MIN), RHO_MAX);
             }
         }
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
@@ -966,9 +983,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         xsol = cold(C_D) * x;
         if (CLOSED && a.wsWarm && t == 0) {
             const bool okst = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
-            a.wsWarm[4 * (size_t)b] = rho;
-            a.wsWarm[4 * (size_t)b + 1] = okst ? 1.0 : 0.0;
-            a.wsWarm[4 * (size_t)b + 2] = (double)(iter > c.max_iter ? c.max_iter : iter);
+            double* wv = a.wsWarm + 4 * (size_t)b;
+            const double w[3] = {rho, okst ? 1.0 : 0.0, (double)(iter > c.max_iter ? c.max_iter : iter)};
+            for (int i = 0; i < 3; ++i) {
+                if (FUSED) st_coh(wv + i, w[i]);
+                else wv[i] = w[i];
+            }
         }
         if (pol_open) toc(cyc_pol);
         stamp(8, nfact);
@@ -981,8 +1001,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         status = early;
         iter = 0;
         if (CLOSED && a.wsWarm && t == 0) {
-            a.wsWarm[4 * (size_t)b + 1] = 0.0;
-            a.wsWarm[4 * (size_t)b + 2] = 0.0;
+            if (FUSED) {
+                st_coh(a.wsWarm + 4 * (size_t)b + 1, 0.0);
+                st_coh(a.wsWarm + 4 * (size_t)b + 2, 0.0);
+            } else {
+                a.wsWarm[4 * (size_t)b + 1] = 0.0;
+                a.wsWarm[4 * (size_t)b + 2] = 0.0;
+            }
         }
     }
 
@@ -1037,11 +1062,17 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             f_cont(p, xs, u, f);
             for (int i = 0; i < 6; ++i) {
                 double xn = xs[i] + Ts * f[i];
-                a.x_state[6 * b + i] = xn;
+                if (FUSED) st_coh(a.x_state + 6 * b + i, xn);
+                else a.x_state[6 * b + i] = xn;
                 if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + tstep + 1) * 6 + i] = xn;
             }
-            a.u_state[2 * b] = uc0;
-            a.u_state[2 * b + 1] = uc1;
+            if (FUSED) {
+                st_coh(a.u_state + 2 * b, uc0);
+                st_coh(a.u_state + 2 * b + 1, uc1);
+            } else {
+                a.u_state[2 * b] = uc0;
+                a.u_state[2 * b + 1] = uc1;
+            }
 
             if (a.hist_u) {
                 a.hist_u[((size_t)b * a.hist_T + tstep) * 2] = uc0;
@@ -1053,12 +1084,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 // mean iterations per step of this launch (the next launch's order), accumulated
                 if (a.wsWarm) {
                     double* m = a.wsWarm + 4 * (size_t)b + 3;
-                    const double acc = (step == 0 ? 0.0 : *m) + iter;
-                    *m = (step == a.nsteps - 1) ? acc / a.nsteps : acc;
+                    const double acc = (step == 0 ? 0.0 : ld_coh(m)) + iter;
+                    st_coh(m, (step == a.nsteps - 1) ? acc / a.nsteps : acc);
                 }
                 if (step == a.nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // launch span
-                // hand the instance to whichever workgroup takes its next step
-                __hip_atomic_store(&a.queue[2 + b], step + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                // hand the instance to whichever workgroup takes its next step: the sc1 state stores
+                // complete (vmcnt(0)), then the step counter is stored sc1 (no L2 writeback)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&a.queue[2 + b], step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();
