@@ -412,7 +412,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
     }
     const float* pa = W2a + (size_t)(hw0 + r) * K + 4 * g;   // h-tile ht: + 16 ht K; chunk c: + 16 c
-    constexpr int NC = K / 16, PD = 2;   // chunks; chunks of W2a loads in flight ahead of the MFMAs
+#ifndef TRAJ_FC2_PD
+#define TRAJ_FC2_PD 2
+#endif
+    constexpr int NC = K / 16, PD = TRAJ_FC2_PD;   // chunks; chunks of W2a loads in flight ahead of the MFMAs
     float4 wa[PD][NT];
 #pragma unroll
     for (int d = 0; d < PD; ++d)
