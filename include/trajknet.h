@@ -105,6 +105,19 @@ int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, con
                        const float* m1x_prior, const float* dy, float* h_sigma, float* x_post, float* out,
                        int out_stride_b, int out_stride_c, float* KG_out, void* stream);
 
+/* back(t) and front(t + 1) fused into one launch (the sequence runner's steady state: 2 launches per
+ * step instead of 3).  Arguments as traj_knet_back_f32 (ws of step t, out column t; no KG_out) and
+ * traj_knet_front_f32 (u, y of step t + 1); h_sigma, x_post, m1x_prior, dy and x2 are updated through
+ * step t and then overwritten with step t + 1's values, h_q / h_s advanced to step t + 1.  Results are
+ * bit-identical to the two separate launches. */
+int traj_knet_back_front_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts,
+                             const traj_knet_net* net, const float* packed, int B, const float* ws, float* out,
+                             int out_stride_b, int out_stride_c, const float* u, int u_stride_b, int u_stride_c,
+                             const float* y, int y_stride_b, int y_stride_c, const float* x_mean, const float* x_std,
+                             const float* y_mean, const float* y_std, const float* u_mean, const float* u_std,
+                             float* h_q, float* h_sigma, float* h_s, float* x_post, float* m1x_prior, float* dy,
+                             float* x2, void* stream);
+
 /* Build-defined EKF baseline for config 5 ("MSE vs reference EKF"; the reference has no EKF, SURVEY.md
  * 8(f) f2), float64, one thread per sequence, all T steps in one launch:
  *   predict  x- = f(x+, u_t) (the clamped vehicle_model.py:109-134 step), F = df/dx by central

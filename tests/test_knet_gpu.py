@@ -115,6 +115,9 @@ def test_fused_runner_vs_oracle(gpu, B, T, groups):
     f2 = run.run(y, u, m1x0, fused=True).cpu().numpy()       # graph replay
     np.testing.assert_array_equal(f1, f0)
     np.testing.assert_array_equal(f2, f0)
+    # back(t) + front(t + 1) merged into one launch == the two launches, bit for bit
+    fs = KNetSequenceRunner(model, B, groups=groups, merge=False).run(y, u, m1x0, fused=True).cpu().numpy()
+    np.testing.assert_array_equal(fs, f0)
     p = dict(KO.PARAMS)
     p.update(LIMITS)
     ref = KO.run_sequences(knet_weights(1), p, float(G["Ts"]), y.cpu().numpy(), u.cpu().numpy(), m1x0.cpu().numpy(),

@@ -120,6 +120,10 @@ _SIGS = {
     "traj_knet_fc2_f32": (C.c_int, [C.POINTER(KnetNet), C.c_int, _V, _V, C.c_size_t, _V]),
     "traj_knet_back_f32": (C.c_int, [C.POINTER(KnetNet), _V, C.c_int, _V, _V, _V, _V, _V, _V, _V, C.c_int,
                                      C.c_int, _V, _V]),
+    "traj_knet_back_front_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float,
+                                           C.POINTER(KnetNet), _V, C.c_int, _V, _V, C.c_int, C.c_int, _V, C.c_int,
+                                           C.c_int, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V,
+                                           _V, _V, _V, _V]),
     "traj_ekf_run_f64": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_double, C.c_int, C.c_int,
                                    _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,

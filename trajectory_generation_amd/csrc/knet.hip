@@ -301,7 +301,7 @@ __device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT,
     __syncthreads();
 }
 
-__global__ __launch_bounds__(KT) void knet_front_kernel(KP p, traj_knet_limits L, float Ts, KNet net, int B,
+__device__ __forceinline__ void front_body(KP p, traj_knet_limits L, float Ts, KNet net, int B,
                                                         const float* __restrict__ x_post, const float* __restrict__ u,
                                                         int u_sb, int u_sc, const float* __restrict__ y, int y_sb,
                                                         int y_sc, const float* __restrict__ xm,
@@ -510,7 +510,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
 }
 
-__global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const float* __restrict__ x2,
+__device__ __forceinline__ void back_body(KNet net, int B, const float* __restrict__ x2,
                                                        const float* __restrict__ part, int nslab,
                                                        const float* __restrict__ prior, const float* __restrict__ dy,
                                                        float* hSig, float* x_post, float* out, int o_sb, int o_sc,
@@ -571,6 +571,138 @@ __global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const fl
             x_post[6 * b + i] = v;
             if (out) out[(size_t)b * o_sb + (size_t)i * o_sc] = v;
         }
+    }
+}
+
+__global__ __launch_bounds__(KT) void knet_front_kernel(KP p, traj_knet_limits L, float Ts, KNet net, int B,
+                                                        const float* x_post, const float* u, int u_sb, int u_sc,
+                                                        const float* y, int y_sb, int y_sc, const float* xm,
+                                                        const float* xs, const float* ym, const float* ys,
+                                                        const float* um, const float* us, float* hQ, const float* hSig,
+                                                        float* hS, float* prior, float* dy, float* x2) {
+    front_body(p, L, Ts, net, B, x_post, u, u_sb, u_sc, y, y_sb, y_sc, xm, xs, ym, ys, um, us, hQ, hSig, hS, prior, dy,
+               x2);
+}
+
+__global__ __launch_bounds__(KT) void knet_back_kernel(KNet net, int B, const float* x2, const float* part, int nslab,
+                                                       const float* prior, const float* dy, float* hSig, float* x_post,
+                                                       float* out, int o_sb, int o_sc, float* KG_out) {
+    back_body(net, B, x2, part, nslab, prior, dy, hSig, x_post, out, o_sb, o_sc, KG_out);
+}
+
+// back(t) and front(t + 1) in one launch: a workgroup finishes step t of its four sequences and goes
+// straight on to step t + 1 -- one launch and one workgroup start per step fewer, h_Sigma(t) handed
+// over in LDS, and the posterior x_post(t) (it needs FC2's output, not FC3/FC4) plus step t + 1's prior
+// computed by four threads that FC3 leaves idle (units >= d_fc3) while the others run FC3.  Each
+// workgroup reads and writes only its own sequences' rows.  Bit-identical to back(t) + front(t + 1).
+__global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, const float* __restrict__ part,
+                                                             int nslab, float* __restrict__ out, int o_sb, int o_sc,
+                                                             KP p, traj_knet_limits L, float Ts,
+                                                             const float* __restrict__ u, int u_sb, int u_sc,
+                                                             const float* __restrict__ y, int y_sb, int y_sc,
+                                                             const float* __restrict__ xm, const float* __restrict__ xs,
+                                                             const float* __restrict__ ym, const float* __restrict__ ys,
+                                                             const float* __restrict__ um, const float* __restrict__ us,
+                                                             float* __restrict__ hQ, float* __restrict__ hSig,
+                                                             float* __restrict__ hS, float* __restrict__ x_post,
+                                                             float* __restrict__ prior, float* __restrict__ dy,
+                                                             float* __restrict__ x2) {
+    __shared__ __attribute__((aligned(16))) float s_a[(KH + 64) * KS];    // [h_S(t) | KG | 0]: FC3's input
+    __shared__ __attribute__((aligned(16))) float s_b[(KH + 64) * KS];    // [out_Sigma(t) | FC3 | 0]: FC4's input
+    __shared__ __attribute__((aligned(16))) float s_o[KH * KS];           // FC4 output = h_Sigma(t)
+    __shared__ __attribute__((aligned(16))) float s_hq[KH * KS];          // h_Q(t)
+    __shared__ __attribute__((aligned(16))) float s_q[KH * KS];           // h_Q(t + 1)
+    __shared__ __attribute__((aligned(16))) float s_g[KH * KS];           // out_Sigma(t + 1)
+    __shared__ __attribute__((aligned(16))) float s_hs[KH * KS];          // h_S(t + 1)
+    __shared__ __attribute__((aligned(16))) float s_pr[64 * KS];          // prior(t + 1), zero-padded
+    __shared__ __attribute__((aligned(16))) float s_dy[64 * KS];          // innovation(t + 1), zero-padded
+    __shared__ __attribute__((aligned(16))) float s_o5[64 * KS];          // FC5 output, zero-padded
+    __shared__ __attribute__((aligned(16))) float s_c1[64 * KS];          // [FC1 | FC7], zero-padded
+    __shared__ __attribute__((aligned(16))) float s_x[KQ * KH * 6 * KS];  // K-quarter partial sums
+    __shared__ float s_red[KS][32][4];
+    const int t = threadIdx.x, b0 = blockIdx.x * KS;
+    const int nb = min(KS, B - b0);
+    const int nm = net.n * net.m;
+    // ---- staging: x2(t) = [out_Sigma | h_S] and h_Q(t), k-major
+    for (int i = t; i < KS * 2 * KH; i += KT) {
+        const int s = i / (2 * KH), k = i - s * 2 * KH;
+        const float v = (s < nb) ? x2[(size_t)(b0 + s) * 2 * KH + k] : 0.0f;
+        if (k < KH) s_b[k * KS + s] = v;
+        else s_a[(k - KH) * KS + s] = v;
+    }
+    for (int i = t; i < KS * KH; i += KT) {
+        const int s = i / KH, k = i - s * KH;
+        s_hq[k * KS + s] = (s < nb) ? hQ[(size_t)(b0 + s) * KH + k] : 0.0f;
+    }
+    for (int i = t; i < 64 * KS; i += KT) s_b[KH * KS + i] = 0.0f;
+    for (int i = t; i < 32 * KS; i += KT) s_a[(KH + 32) * KS + i] = 0.0f;
+    if (t < 64 * KS) s_o5[t] = s_c1[t] = s_pr[t] = s_dy[t] = 0.0f;
+    {   // KG = b2b + sum over FC2's slabs: thread (s, j, q) sums the slabs sl = q mod 4
+        const int s = t >> 7, j = (t >> 2) & 31, q = t & 3;
+        float a = 0.0f;
+        if (s < nb) {
+            const float* pp = part + ((size_t)b0 + s) * 32 + j;
+#pragma unroll 8
+            for (int sl = q; sl < nslab; sl += 4) a = __fadd_rn(a, pp[(size_t)sl * B * 32]);
+        }
+        s_red[s][j][q] = a;
+    }
+    __syncthreads();
+    if (t < KS * 32) {
+        const int s = t >> 5, j = t & 31;
+        float v = 0.0f;
+        if (j < nm && s < nb)
+            v = __fadd_rn(net.b2b[j], __fadd_rn(__fadd_rn(s_red[s][j][0], s_red[s][j][1]),
+                                                __fadd_rn(s_red[s][j][2], s_red[s][j][3])));
+        s_a[(KH + j) * KS + s] = v;
+    }
+    __syncthreads();
+    // ---- posterior x_post(t) (kalman_net.py:169-178) and step t + 1's prior (:145-162): threads
+    // KT - KS .. KT - 1 (K quarter 3, units 124..127: idle in FC3), overlapping FC3
+    if (t >= KT - KS) {
+        const int s = t - (KT - KS);
+        float pr[6] = {0, 0, 0, 0, 0, 0}, e[5] = {0, 0, 0, 0, 0};
+        if (s < nb) {
+            const int b = b0 + s;
+            const float gamma = sigmoidf_(net.logit[0]);
+            float xp[6];
+            for (int i = 0; i < 6; ++i) {
+                float sacc = 0.0f;
+                for (int j = 0; j < 5; ++j)
+                    sacc = __fadd_rn(sacc, __fmul_rn(s_a[(KH + 5 * i + j) * KS + s], dy[5 * b + j]));
+                xp[i] = __fadd_rn(prior[6 * b + i], __fmul_rn(gamma, sacc));
+                x_post[6 * b + i] = xp[i];
+                out[(size_t)b * o_sb + (size_t)i * o_sc] = xp[i];
+            }
+            prior_one(p, L, Ts, xp, u[(size_t)b * u_sb], u[(size_t)b * u_sb + u_sc], y + (size_t)b * y_sb, y_sc, xm,
+                      xs, ym, ys, um, us, pr, nullptr, e);
+            for (int i = 0; i < 6; ++i) prior[6 * b + i] = pr[i];
+            for (int j = 0; j < 5; ++j) dy[5 * b + j] = e[j];
+        }
+        for (int i = 0; i < 6; ++i) s_pr[i * KS + s] = pr[i];
+        for (int j = 0; j < 5; ++j) s_dy[j * KS + s] = e[j];
+    }
+    // ---- back(t): FC3 + ReLU on cat(h_S, out_FC2); FC4 + ReLU on cat(out_Sigma, out_FC3) = h_Sigma(t)
+    dense_ks(s_a, k4_(KH + nm), net.W3, net.b3, net.dFC3, s_b + KH * KS, true, s_x, t);
+    dense_ks(s_b, k4_(KH + net.dFC3), net.W4, net.b4, KH, s_o, true, s_x, t);
+    for (int i = t; i < nb * KH; i += KT) {
+        const int s = i / KH, k = i - s * KH;
+        hSig[(size_t)(b0 + s) * KH + k] = s_o[k * KS + s];
+    }
+    // ---- front(t + 1): FC5, GRU_Q, GRU_Sigma (on h_Sigma(t) in LDS), FC1, FC7, GRU_S (on h_S(t) = s_a[0, KH))
+    dense_ks(s_pr, k4_(net.m), net.W5, net.b5, net.dFC5, s_o5, true, s_x, t);                    // FC5 + ReLU
+    gru_ks(s_o5, k4_(net.dFC5), s_hq, net.WiQ, net.biQ, net.WhQ, net.bhQ, s_q, s_x, t);          // GRU_Q
+    gru_ks(s_q, KH / 4, s_o, net.WiG, net.biG, net.WhG, net.bhG, s_g, s_x, t);                   // GRU_Sigma
+    dense_ks(s_g, KH / 4, net.W1, net.b1, net.dFC1, s_c1, true, s_x, t);                         // FC1 + ReLU
+    dense_ks(s_dy, k4_(net.n), net.W7, net.b7, net.dFC7, s_c1 + KS * net.dFC1, true, s_x, t);    // FC7 + ReLU
+    gru_ks(s_c1, k4_(net.dFC1 + net.dFC7), s_a, net.WiS, net.biS, net.WhS, net.bhS, s_hs, s_x, t);   // GRU_S
+    for (int i = t; i < nb * KH; i += KT) {
+        const int s = i / KH, k = i - s * KH;
+        const size_t b = (size_t)(b0 + s);
+        hQ[b * KH + k] = s_q[k * KS + s];
+        hS[b * KH + k] = s_hs[k * KS + s];
+        x2[b * 2 * KH + k] = s_g[k * KS + s];
+        x2[b * 2 * KH + KH + k] = s_hs[k * KS + s];
     }
 }
 
@@ -839,6 +971,30 @@ int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, con
     hipLaunchKernelGGL(knet_back_kernel, dim3(nblk(B, KS)), dim3(KT), 0, (hipStream_t)stream, knet_args(net, packed),
                        B, x2, ws, net->d_fc2h / fc2_slab(net->d_fc2h), m1x_prior, dy, h_sigma, x_post, out, out_stride_b,
                        out_stride_c, KG_out);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_knet_back_front_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts,
+                             const traj_knet_net* net, const float* packed, int B, const float* ws, float* out,
+                             int out_stride_b, int out_stride_c, const float* u, int u_stride_b, int u_stride_c,
+                             const float* y, int y_stride_b, int y_stride_c, const float* x_mean, const float* x_std,
+                             const float* y_mean, const float* y_std, const float* u_mean, const float* u_std,
+                             float* h_q, float* h_sigma, float* h_s, float* x_post, float* m1x_prior, float* dy,
+                             float* x2, void* stream) {
+    if (!p || !lim || B < 0) return TRAJ_E_ARG;
+    if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!packed || ((uintptr_t)packed & 15) || !ws || !u || !y || !x_mean || !x_std || !y_mean || !y_std || !h_q ||
+        !h_sigma || !h_s || !x_post || !m1x_prior || !dy || !x2)
+        return TRAJ_E_ARG;
+    KP k{(float)p->Cm1, (float)p->Cm2, (float)p->Cr0, (float)p->Cr2, (float)p->Br, (float)p->Cr, (float)p->Dr,
+         (float)p->Bf,  (float)p->Cf,  (float)p->Df,  (float)p->m,   (float)p->Iz, (float)p->lf, (float)p->lr,
+         (float)p->maxAlpha, (float)p->vx_zero};
+    if (!out) return TRAJ_E_ARG;
+    hipLaunchKernelGGL(knet_back_front_kernel, dim3(nblk(B, KS)), dim3(KT), 0, (hipStream_t)stream,
+                       knet_args(net, packed), B, ws, net->d_fc2h / fc2_slab(net->d_fc2h), out, out_stride_b,
+                       out_stride_c, k, *lim, Ts, u, u_stride_b, u_stride_c, y, y_stride_b, y_stride_c, x_mean, x_std,
+                       y_mean, y_std, u_mean, u_std, h_q, h_sigma, h_s, x_post, m1x_prior, dy, x2);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 

@@ -12,10 +12,11 @@ its checkpoints load unchanged.  What runs on the device per step (kalman_net.py
 * ``traj_knet_update_f32`` (HIP) x_post = x_prior + sigmoid(innov_logit) * KG dy (:169-178).
 
 ``KNetSequenceRunner`` captures one whole step in a HIP graph and replays it T times; its fused mode
-(the throughput path) runs a step as three launches -- ``traj_knet_front_f32`` (prior + FC5 + the three
-GRU cells + FC1/FC7 for four sequences per workgroup), ``traj_knet_fc2_f32`` (FC2 on the f32 matrix
-cores, its [B, 10240] hidden activation kept on chip), ``traj_knet_back_f32`` (FC3 + FC4 + posterior
-update) -- and captures all T steps in one graph.
+(the throughput path) runs a step as ``traj_knet_front_f32`` (prior + FC5 + the three GRU cells + FC1/FC7
+for four sequences per workgroup), ``traj_knet_fc2_f32`` (FC2 on the f32 matrix cores, its [B, 10240]
+hidden activation kept on chip) and ``traj_knet_back_f32`` (FC3 + FC4 + posterior update), with back(t)
+and front(t + 1) fused into one launch (``traj_knet_back_front_f32``), and captures all T steps in one
+graph.
 There is no CPU path: the ops raise without the HIP library or a GPU.
 
 Training (``knet_train.py``): with autograd on, the three HIP ops run inside
@@ -415,10 +416,12 @@ class KNetSequenceRunner:
     Mirrors the inference loop of training_prediction.py:118-137 / test_vehicle.py:123-145:
     init_hidden_KNet, InitSequence(m1x0), then forward(y[:, :, t], u[:, :, t]) for t < T."""
 
-    def __init__(self, model: KalmanNetNN, B: int, groups: int = 1):
+    def __init__(self, model: KalmanNetNN, B: int, groups: int = 1, merge: bool = True):
         """groups: the fused mode's sequences split into that many independent launch chains (graph
-        branches), so one group's latency-bound GRU kernels overlap another's FC2 on the matrix cores."""
-        self.model, self.B, self.groups = model, B, groups
+        branches), so one group's latency-bound GRU kernels overlap another's FC2 on the matrix cores.
+        merge: back(t) and front(t + 1) as one launch (traj_knet_back_front_f32); False keeps them apart
+        (bit-identical results; for tests)."""
+        self.model, self.B, self.groups, self.merge = model, B, groups, merge
         dev = model.device
         self.y = torch.zeros((B, model.n, 1), device=dev)
         self.u = torch.zeros((B, 2, 1), device=dev)
@@ -441,19 +444,35 @@ class KNetSequenceRunner:
         Bg, ws = r1 - r0, S["ws"][g]
         row = lambda key, width: C.c_void_p(S[key].data_ptr() + 4 * r0 * width)   # noqa: E731
         net, pk = C.byref(S["net"]), _p(S["pk"])
+        ucol = lambda t: C.c_void_p(S["u"].data_ptr() + 4 * (r0 * 2 * T + t))   # noqa: E731
+        ycol = lambda t: C.c_void_p(S["y"].data_ptr() + 4 * (r0 * n * T + t))   # noqa: E731
+        ocol = lambda t: C.c_void_p(S["out"].data_ptr() + 4 * (r0 * m * T + t))   # noqa: E731
+        norm = [_p(xm), _p(xs), _p(ym), _p(ys), _p(S["um"]), _p(S["us"])]
+        # step t = fc2(t), then back(t) fused with front(t + 1): two launches per step after the first
         for t in range(steps):
-            _lib.check(L.traj_knet_front_f32(
-                C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, row("post", m),
-                C.c_void_p(S["u"].data_ptr() + 4 * (r0 * 2 * T + t)), 2 * T, T,
-                C.c_void_p(S["y"].data_ptr() + 4 * (r0 * n * T + t)), n * T, T,
-                _p(xm), _p(xs), _p(ym), _p(ys), _p(S["um"]), _p(S["us"]), row("hQ", H), row("hSig", H), row("hS", H),
-                row("prior", m), row("dy", n), row("x2", 2 * H), _stream()), "traj_knet_front_f32")
+            if t == 0:
+                _lib.check(L.traj_knet_front_f32(
+                    C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, row("post", m),
+                    ucol(0), 2 * T, T, ycol(0), n * T, T, *norm, row("hQ", H), row("hSig", H), row("hS", H),
+                    row("prior", m), row("dy", n), row("x2", 2 * H), _stream()), "traj_knet_front_f32")
             _lib.check(L.traj_knet_fc2_f32(net, Bg, row("x2", 2 * H), _p(ws), ws.numel() * 4, _stream()),
                        "traj_knet_fc2_f32")
-            _lib.check(L.traj_knet_back_f32(
-                net, pk, Bg, row("x2", 2 * H), _p(ws), row("prior", m), row("dy", n), row("hSig", H),
-                row("post", m), C.c_void_p(S["out"].data_ptr() + 4 * (r0 * m * T + t)), m * T, T, None, _stream()),
-                "traj_knet_back_f32")
+            if t + 1 < steps and self.merge:
+                _lib.check(L.traj_knet_back_front_f32(
+                    C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, _p(ws), ocol(t), m * T, T,
+                    ucol(t + 1), 2 * T, T, ycol(t + 1), n * T, T, *norm, row("hQ", H), row("hSig", H), row("hS", H),
+                    row("post", m), row("prior", m), row("dy", n), row("x2", 2 * H), _stream()),
+                    "traj_knet_back_front_f32")
+            else:
+                _lib.check(L.traj_knet_back_f32(
+                    net, pk, Bg, row("x2", 2 * H), _p(ws), row("prior", m), row("dy", n), row("hSig", H),
+                    row("post", m), ocol(t), m * T, T, None, _stream()), "traj_knet_back_f32")
+                if t + 1 < steps:
+                    _lib.check(L.traj_knet_front_f32(
+                        C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, row("post", m),
+                        ucol(t + 1), 2 * T, T, ycol(t + 1), n * T, T, *norm, row("hQ", H), row("hSig", H),
+                        row("hS", H), row("prior", m), row("dy", n), row("x2", 2 * H), _stream()),
+                        "traj_knet_front_f32")
 
     def _enqueue_all(self, T, steps):
         """All row groups' steps; groups > 1 run as independent chains on side streams (graph branches)."""
