@@ -39,6 +39,8 @@ from trajectory_generation_amd import batch as TB  # noqa: E402
 from trajectory_generation_amd.workload import make_workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+F64_VECTOR_PEAK_TF = 78.6   # MI355X FP64 vector spec (AMD product sheet; the guide lists no f64 figure)
+SIMDS, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs, max clock (MI355X_MICROARCH.md chip table)
 
 
 def algorithmic_bytes_per_traj(N: int, kmax: int) -> int:
@@ -194,6 +196,8 @@ def main():
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r01.json"),
+                    help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
     ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r01.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
     args = ap.parse_args()
@@ -287,6 +291,23 @@ def main():
                     traffic_step = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = traffic_step = None
+    issue = None
+    if os.path.exists(args.issue_json):
+        try:
+            with open(args.issue_json) as f:
+                ij = json.load(f)
+            if ij.get("batch") == B and N == 20:
+                # solve_kernel is VALU-issue/latency bound: the issued f64 lane-FLOP rate against the f64
+                # vector peak, and the VALU issue slots used (4 cycles per wave64 instruction)
+                fl = ij["f64_flop_issued_per_step"] * value / world / 1e12
+                issue = {"what": "solve_kernel issue side (PMC SQ_INSTS_VALU*, per instance-step x steps/s)",
+                         "f64_tflops_issued": fl, "f64_peak_tflops": F64_VECTOR_PEAK_TF,
+                         "f64_frac": fl / F64_VECTOR_PEAK_TF,
+                         "valu_insts_per_step": ij["valu_insts_per_step"],
+                         "valu_issue_frac": ij["valu_insts_per_step"] * 4 * value / world / (SIMDS * CLOCK_HZ),
+                         "source": os.path.relpath(args.issue_json, HERE)}
+        except (OSError, ValueError, KeyError):
+            issue = None
     out = {
         "metric": "MPC steps/sec (batch=4096, N=20)" if (B == 4096 and N == 20) else f"MPC steps/sec (batch={B}, N={N})",
         "value": value,
@@ -310,7 +331,8 @@ def main():
                          f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
                      "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
                      "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,
-                     "traffic_source": os.path.relpath(args.traffic_json, HERE) if traffic is not None else None},
+                     "traffic_source": os.path.relpath(args.traffic_json, HERE) if traffic is not None else None,
+                     "issue": issue},
         "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
                          "iters_max": int(iters.max()),
                          "status_hist": np.bincount(stat, minlength=7).tolist()},

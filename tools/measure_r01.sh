@@ -15,8 +15,10 @@ python3 tools/pmc_traffic.py --fetch gpurun_out/prof_fetch --write gpurun_out/pr
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/kprof_fetch -o run --output-format csv -- python3 tools/knet_pmc_run.py > gpurun_out/kprof_fetch.log 2>&1 &&
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/kprof_write -o run --output-format csv -- python3 tools/knet_pmc_run.py > gpurun_out/kprof_write.log 2>&1 &&
 python3 tools/pmc_knet_traffic.py --fetch gpurun_out/kprof_fetch --write gpurun_out/kprof_write --batch 1024 --out gpurun_out/traffic_knet_r01.json > /dev/null &&
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAVES -d gpurun_out/pmc_f64 -o run --output-format csv -- python3 bench.py --no-cpu --no-knet --steps 20 > gpurun_out/pmc_f64.log 2>&1 &&
+python3 tools/pmc_f64.py gpurun_out/pmc_f64 --batch 4096 --steps-per-launch 20 --out gpurun_out/sq_f64_r01.json > /dev/null &&
 echo pmc ok &&
-timeout -k 10 300 python bench.py --traffic-json gpurun_out/traffic_r01.json --knet-traffic-json gpurun_out/traffic_knet_r01.json > gpurun_out/bench.json 2> gpurun_out/bench.err &&
+timeout -k 10 300 python bench.py --traffic-json gpurun_out/traffic_r01.json --knet-traffic-json gpurun_out/traffic_knet_r01.json --issue-json gpurun_out/sq_f64_r01.json > gpurun_out/bench.json 2> gpurun_out/bench.err &&
 echo bench ok &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_kt -o run --output-format csv -- python3 bench.py --no-cpu > gpurun_out/prof_kt.log 2>&1 &&
 python3 tools/trace_dispatches.py gpurun_out/prof_kt/run_kernel_trace.csv "solve_kernel<40, true, true>" gpurun_out/solve_dispatches.json > /dev/null &&
