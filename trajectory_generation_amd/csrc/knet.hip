@@ -224,11 +224,35 @@ __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const 
 
 constexpr int K4_H = KH / 4;   // rows of 4 of every W_hh
 
+struct NoSide {
+    __device__ void operator()() const {}
+};
+
+// One output of a small dense layer (K <= 16: the whole row in quarter 0 of dense_ks) by a single
+// thread, bit-identical to dense_ks: the fmaf chain in k order from the bias, then the three zero
+// partials of the other quarters (which turn a -0 into +0), then ReLU.  P: packed as dense_ks reads it.
+__device__ __forceinline__ float dense_one(const float* xT, int K, const float4* __restrict__ P,
+                                           const float* __restrict__ bias, int N, int j, int s) {
+    float acc = bias[j];
+    for (int k4 = 0; 4 * k4 < K; ++k4) {
+        const float4 w = P[(size_t)k4 * N + j];
+        const float* x = xT + 4 * KS * k4 + s;
+        acc = fmaf(x[0], w.x, acc);
+        if (4 * k4 + 1 < K) acc = fmaf(x[KS], w.y, acc);
+        if (4 * k4 + 2 < K) acc = fmaf(x[2 * KS], w.z, acc);
+        if (4 * k4 + 3 < K) acc = fmaf(x[3 * KS], w.w, acc);
+    }
+    return fmaxf(__fadd_rn(acc, 0.0f), 0.0f);
+}
+
 // Dense layer: outT[j][s] = act(b[j] + sum_k xT[k][s] W[j][k]) for j < N <= KH (outT: LDS, k-major).
-// xch: LDS scratch of (KQ - 1) * KH * KS floats.  Called by every thread of the workgroup.
+// xch: LDS scratch of (KQ - 1) * KH * KS floats.  Called by every thread of the workgroup.  `side` runs
+// on every thread between the two barriers (after the partial sums are published, while quarter 0
+// finishes): work for the threads the layer leaves idle there (units >= N).
+template <class Side = NoSide>
 __device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* __restrict__ P,
                                          const float* __restrict__ bias, int N, float* outT, bool relu, float* xch,
-                                         int t) {
+                                         int t, Side side = {}) {
     const int j = t & (KH - 1), part = t >> 7, h4 = K4 / KQ;
     float acc[1][KS] = {{0.0f, 0.0f, 0.0f, 0.0f}};
     if (j < N) {
@@ -239,6 +263,7 @@ __device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* 
                 make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
     }
     __syncthreads();
+    side();
     if (j < N && part == 0) {
         float4 r = make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
 #pragma unroll
@@ -682,19 +707,35 @@ __global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, co
         for (int i = 0; i < 6; ++i) s_pr[i * KS + s] = pr[i];
         for (int j = 0; j < 5; ++j) s_dy[j * KS + s] = e[j];
     }
-    // ---- back(t): FC3 + ReLU on cat(h_S, out_FC2); FC4 + ReLU on cat(out_Sigma, out_FC3) = h_Sigma(t)
-    dense_ks(s_a, k4_(KH + nm), net.W3, net.b3, net.dFC3, s_b + KH * KS, true, s_x, t);
+    // ---- back(t): FC3 + ReLU on cat(h_S, out_FC2); FC4 + ReLU on cat(out_Sigma, out_FC3) = h_Sigma(t).
+    // FC3 has at most 64 units, so units 64..127 are idle once its partials are published: there they
+    // run step t + 1's FC5 (on the prior) and FC7 (on the innovation), one output per thread, instead of
+    // two more layer stages after FC4.
+    const bool side = net.dFC3 <= 64 && net.m <= 16 && net.n <= 16 && (net.dFC5 + net.dFC7) * KS <= 4 * KT / 2;
+    auto fc57 = [&]() {
+        if (!side || (t & (KH - 1)) < 64) return;
+        const int i = (t >> 7) * 64 + (t & 63);
+        for (int o = i; o < (net.dFC5 + net.dFC7) * KS; o += KT / 2) {
+            const int s = o & (KS - 1), unit = o / KS;
+            if (unit < net.dFC5) s_o5[unit * KS + s] = dense_one(s_pr, net.m, net.W5, net.b5, net.dFC5, unit, s);
+            else {
+                const int v = unit - net.dFC5;
+                s_c1[(net.dFC1 + v) * KS + s] = dense_one(s_dy, net.n, net.W7, net.b7, net.dFC7, v, s);
+            }
+        }
+    };
+    dense_ks(s_a, k4_(KH + nm), net.W3, net.b3, net.dFC3, s_b + KH * KS, true, s_x, t, fc57);
     dense_ks(s_b, k4_(KH + net.dFC3), net.W4, net.b4, KH, s_o, true, s_x, t);
     for (int i = t; i < nb * KH; i += KT) {
         const int s = i / KH, k = i - s * KH;
         hSig[(size_t)(b0 + s) * KH + k] = s_o[k * KS + s];
     }
     // ---- front(t + 1): FC5, GRU_Q, GRU_Sigma (on h_Sigma(t) in LDS), FC1, FC7, GRU_S (on h_S(t) = s_a[0, KH))
-    dense_ks(s_pr, k4_(net.m), net.W5, net.b5, net.dFC5, s_o5, true, s_x, t);                    // FC5 + ReLU
+    if (!side) dense_ks(s_pr, k4_(net.m), net.W5, net.b5, net.dFC5, s_o5, true, s_x, t);        // FC5 + ReLU
     gru_ks(s_o5, k4_(net.dFC5), s_hq, net.WiQ, net.biQ, net.WhQ, net.bhQ, s_q, s_x, t);          // GRU_Q
     gru_ks(s_q, KH / 4, s_o, net.WiG, net.biG, net.WhG, net.bhG, s_g, s_x, t);                   // GRU_Sigma
     dense_ks(s_g, KH / 4, net.W1, net.b1, net.dFC1, s_c1, true, s_x, t);                         // FC1 + ReLU
-    dense_ks(s_dy, k4_(net.n), net.W7, net.b7, net.dFC7, s_c1 + KS * net.dFC1, true, s_x, t);    // FC7 + ReLU
+    if (!side) dense_ks(s_dy, k4_(net.n), net.W7, net.b7, net.dFC7, s_c1 + KS * net.dFC1, true, s_x, t);   // FC7
     gru_ks(s_c1, k4_(net.dFC1 + net.dFC7), s_a, net.WiS, net.biS, net.WhS, net.bhS, s_hs, s_x, t);   // GRU_S
     for (int i = t; i < nb * KH; i += KT) {
         const int s = i / KH, k = i - s * KH;
