@@ -224,6 +224,13 @@ __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const 
 
 constexpr int K4_H = KH / 4;   // rows of 4 of every W_hh
 
+// Timing experiments only (tools/knet_bf_stages.sh): TRAJ_BF_SKIP bit i drops stage i of
+// knet_back_front_kernel (wrong results).  0 in every shipped build.
+#ifndef TRAJ_BF_SKIP
+#define TRAJ_BF_SKIP 0
+#endif
+#define BF_RUN(i) ((TRAJ_BF_SKIP & (1 << (i))) == 0)
+
 struct NoSide {
     __device__ void operator()() const {}
 };
@@ -249,6 +256,35 @@ __device__ __forceinline__ float dense_one(const float* xT, int K, const float4*
 // xch: LDS scratch of (KQ - 1) * KH * KS floats.  Called by every thread of the workgroup.  `side` runs
 // on every thread between the two barriers (after the partial sums are published, while quarter 0
 // finishes): work for the threads the layer leaves idle there (units >= N).
+// First half of dense_ks: quarter `part` of unit j's dot product; quarters 1..3 publish their partial
+// to xch, quarter 0 keeps it (returned) for dense_finish after the barrier.
+__device__ __forceinline__ float4 dense_publish(const float* xT, int K4, const float4* __restrict__ P,
+                                                const float* __restrict__ bias, int N, float* xch, int t) {
+    const int j = t & (KH - 1), part = t >> 7, h4 = K4 / KQ;
+    float acc[1][KS] = {{0.0f, 0.0f, 0.0f, 0.0f}};
+    if (j < N) {
+        if (part == 0) acc[0][0] = acc[0][1] = acc[0][2] = acc[0][3] = bias[j];
+        dot_ks<1>(xT, part * h4, (part + 1) * h4, P, N, j, acc);
+        if (part)
+            *reinterpret_cast<float4*>(xch + ((part - 1) * KH + j) * KS) =
+                make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+    }
+    return make_float4(acc[0][0], acc[0][1], acc[0][2], acc[0][3]);
+}
+
+__device__ __forceinline__ void dense_finish(float4 r, int N, float* outT, bool relu, const float* xch, int t) {
+    const int j = t & (KH - 1), part = t >> 7;
+    if (j < N && part == 0) {
+#pragma unroll
+        for (int q = 1; q < KQ; ++q) {
+            const float4 o = *reinterpret_cast<const float4*>(xch + ((q - 1) * KH + j) * KS);
+            r = make_float4(__fadd_rn(r.x, o.x), __fadd_rn(r.y, o.y), __fadd_rn(r.z, o.z), __fadd_rn(r.w, o.w));
+        }
+        if (relu) r = make_float4(fmaxf(r.x, 0.0f), fmaxf(r.y, 0.0f), fmaxf(r.z, 0.0f), fmaxf(r.w, 0.0f));
+        *reinterpret_cast<float4*>(outT + KS * j) = r;
+    }
+}
+
 template <class Side = NoSide>
 __device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* __restrict__ P,
                                          const float* __restrict__ bias, int N, float* outT, bool relu, float* xch,
@@ -281,9 +317,9 @@ __device__ __forceinline__ void dense_ks(const float* xT, int K4, const float4* 
 // Thread (unit u, quarter q) forms its quarter's partial gates for all KS sequences, then finishes
 // sequence q from the four quarters' partials (added in quarter order).  xch: LDS scratch of
 // KQ * KH * 6 * KS floats.
-__device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT, const float4* __restrict__ Wi,
-                                       const float* __restrict__ bi, const float4* __restrict__ Wh,
-                                       const float* __restrict__ bh, float* houtT, float* xch, int t) {
+__device__ __forceinline__ void gru_publish(const float* xT, int K4, const float* hT, const float4* __restrict__ Wi,
+                                            const float* __restrict__ bi, const float4* __restrict__ Wh,
+                                            const float* __restrict__ bh, float* xch, int t) {
     static_assert(KQ == KS, "one finished sequence per K quarter");
     const int u = t & (KH - 1), part = t >> 7;
     float gi[3][KS], gh[3][KS];
@@ -305,7 +341,12 @@ __device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT,
         *reinterpret_cast<float2*>(mine + 6 * q + 2) = make_float2(gi[2][q], gh[0][q]);
         *reinterpret_cast<float2*>(mine + 6 * q + 4) = make_float2(gh[1][q], gh[2][q]);
     }
-    __syncthreads();
+}
+
+// Second half of the GRU cell (after a barrier that follows gru_publish): thread (unit u, quarter q)
+// adds the four quarters' partials of sequence q in quarter order and applies the gates.
+__device__ __forceinline__ void gru_finish(const float* hT, float* houtT, const float* xch, int t) {
+    const int u = t & (KH - 1), part = t >> 7;
     const int sq = part;   // the sequence this thread finishes
     float ir[3] = {0.0f, 0.0f, 0.0f}, hr[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -323,6 +364,14 @@ __device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT,
     const float nn = tanhf(__fadd_rn(ir[2], __fmul_rn(hr[2], r)));
     const float hv = hT[u * KS + sq];
     houtT[u * KS + sq] = __fadd_rn(__fmul_rn(__fsub_rn(hv, nn), z), nn);
+}
+
+__device__ __forceinline__ void gru_ks(const float* xT, int K4, const float* hT, const float4* __restrict__ Wi,
+                                       const float* __restrict__ bi, const float4* __restrict__ Wh,
+                                       const float* __restrict__ bh, float* houtT, float* xch, int t) {
+    gru_publish(xT, K4, hT, Wi, bi, Wh, bh, xch, t);
+    __syncthreads();
+    gru_finish(hT, houtT, xch, t);
     __syncthreads();
 }
 
@@ -645,6 +694,7 @@ __global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, co
     __shared__ __attribute__((aligned(16))) float s_c1[64 * KS];          // [FC1 | FC7], zero-padded
     __shared__ __attribute__((aligned(16))) float s_x[KQ * KH * 6 * KS];  // K-quarter partial sums
     __shared__ float s_red[KS][32][4];
+    __shared__ __attribute__((aligned(16))) float s_x4[(KQ - 1) * KH * KS];  // FC4's partials (beside GRU_Q's)
     const int t = threadIdx.x, b0 = blockIdx.x * KS;
     const int nb = min(KS, B - b0);
     const int nm = net.n * net.m;
@@ -667,8 +717,9 @@ __global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, co
         float a = 0.0f;
         if (s < nb) {
             const float* pp = part + ((size_t)b0 + s) * 32 + j;
+            if (BF_RUN(0))
 #pragma unroll 8
-            for (int sl = q; sl < nslab; sl += 4) a = __fadd_rn(a, pp[(size_t)sl * B * 32]);
+                for (int sl = q; sl < nslab; sl += 4) a = __fadd_rn(a, pp[(size_t)sl * B * 32]);
         }
         s_red[s][j][q] = a;
     }
@@ -687,7 +738,7 @@ __global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, co
     if (t >= KT - KS) {
         const int s = t - (KT - KS);
         float pr[6] = {0, 0, 0, 0, 0, 0}, e[5] = {0, 0, 0, 0, 0};
-        if (s < nb) {
+        if (s < nb && BF_RUN(1)) {
             const int b = b0 + s;
             const float gamma = sigmoidf_(net.logit[0]);
             float xp[6];
@@ -724,19 +775,30 @@ __global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, co
             }
         }
     };
-    dense_ks(s_a, k4_(KH + nm), net.W3, net.b3, net.dFC3, s_b + KH * KS, true, s_x, t, fc57);
-    dense_ks(s_b, k4_(KH + net.dFC3), net.W4, net.b4, KH, s_o, true, s_x, t);
+    if (BF_RUN(2)) dense_ks(s_a, k4_(KH + nm), net.W3, net.b3, net.dFC3, s_b + KH * KS, true, s_x, t, fc57);
+    // ---- front(t + 1): FC5, GRU_Q, GRU_Sigma (on h_Sigma(t) in LDS), FC1, FC7, GRU_S (on h_S(t) = s_a[0, KH)).
+    // With FC5 done above, GRU_Q(t + 1) does not wait for FC4(t): the two share one stage (both
+    // publish their quarter partials, one barrier, both finish).
+    if (side && BF_RUN(3)) {
+        const float4 r4 = dense_publish(s_b, k4_(KH + net.dFC3), net.W4, net.b4, KH, s_x4, t);
+        gru_publish(s_o5, k4_(net.dFC5), s_hq, net.WiQ, net.biQ, net.WhQ, net.bhQ, s_x, t);
+        __syncthreads();
+        dense_finish(r4, KH, s_o, true, s_x4, t);
+        gru_finish(s_hq, s_q, s_x, t);
+        __syncthreads();
+    } else if (!side) {
+        dense_ks(s_b, k4_(KH + net.dFC3), net.W4, net.b4, KH, s_o, true, s_x, t);
+        dense_ks(s_pr, k4_(net.m), net.W5, net.b5, net.dFC5, s_o5, true, s_x, t);                // FC5 + ReLU
+        gru_ks(s_o5, k4_(net.dFC5), s_hq, net.WiQ, net.biQ, net.WhQ, net.bhQ, s_q, s_x, t);      // GRU_Q
+    }
     for (int i = t; i < nb * KH; i += KT) {
         const int s = i / KH, k = i - s * KH;
         hSig[(size_t)(b0 + s) * KH + k] = s_o[k * KS + s];
     }
-    // ---- front(t + 1): FC5, GRU_Q, GRU_Sigma (on h_Sigma(t) in LDS), FC1, FC7, GRU_S (on h_S(t) = s_a[0, KH))
-    if (!side) dense_ks(s_pr, k4_(net.m), net.W5, net.b5, net.dFC5, s_o5, true, s_x, t);        // FC5 + ReLU
-    gru_ks(s_o5, k4_(net.dFC5), s_hq, net.WiQ, net.biQ, net.WhQ, net.bhQ, s_q, s_x, t);          // GRU_Q
-    gru_ks(s_q, KH / 4, s_o, net.WiG, net.biG, net.WhG, net.bhG, s_g, s_x, t);                   // GRU_Sigma
-    dense_ks(s_g, KH / 4, net.W1, net.b1, net.dFC1, s_c1, true, s_x, t);                         // FC1 + ReLU
+    if (BF_RUN(4)) gru_ks(s_q, KH / 4, s_o, net.WiG, net.biG, net.WhG, net.bhG, s_g, s_x, t);     // GRU_Sigma
+    if (BF_RUN(5)) dense_ks(s_g, KH / 4, net.W1, net.b1, net.dFC1, s_c1, true, s_x, t);           // FC1 + ReLU
     if (!side) dense_ks(s_dy, k4_(net.n), net.W7, net.b7, net.dFC7, s_c1 + KS * net.dFC1, true, s_x, t);   // FC7
-    gru_ks(s_c1, k4_(net.dFC1 + net.dFC7), s_a, net.WiS, net.biS, net.WhS, net.bhS, s_hs, s_x, t);   // GRU_S
+    if (BF_RUN(6)) gru_ks(s_c1, k4_(net.dFC1 + net.dFC7), s_a, net.WiS, net.biS, net.WhS, net.bhS, s_hs, s_x, t);  // GRU_S
     for (int i = t; i < nb * KH; i += KT) {
         const int s = i / KH, k = i - s * KH;
         const size_t b = (size_t)(b0 + s);
