@@ -50,6 +50,7 @@ class OrcCfg(C.Structure):
         ("adaptive_rho_tol", C.c_double),
         ("polish_mode", C.c_int), ("polish_max_pass", C.c_int), ("cert_tol", C.c_double),
         ("polish_max_rounds", C.c_int), ("warm_start", C.c_int),
+        ("solver", C.c_int), ("ipm_max_iter", C.c_int), ("ipm_tol", C.c_double),
     ]
 
 
@@ -95,6 +96,8 @@ def lib():
                                          _I, _D, _D, _D, _I, _I, C.c_int]
         L.orc_qp_exact.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), _D, _D, _D, _D, _D, _D]
         L.orc_qp_exact.restype = C.c_int
+        L.orc_qp_ipm.argtypes = [C.POINTER(OrcCfg), _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, C.POINTER(OrcInfo)]
+        L.orc_qp_ipm.restype = C.c_int
         L.orc_d_steady_state.argtypes = [C.POINTER(OrcParams), C.c_double]
         L.orc_d_steady_state.restype = C.c_double
         L.orc_vref_ramp.argtypes = [C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, _D]
@@ -247,6 +250,22 @@ def qp_exact(x0, u_prev, path_ref, vref, c: OrcCfg, p=None):
     rc = lib().orc_qp_exact(C.byref(p), C.byref(c), _dp(_f64(x0, 6)), _dp(_f64(u_prev, 2)),
                             _dp(_f64(path_ref, (N + 1, 3))), _dp(_f64(vref, N + 1)), _dp(U), C.byref(obj))
     return (U, obj.value) if rc == 0 else None
+
+
+def qp_ipm(x0, u_prev, path_ref, vref, Ad, Bd, g, c: OrcCfg, xinit=None):
+    """The QP half (mpc_6stati.py:180-275) in its sparse form by the structured interior-point method
+    (riccati_ipm.c) with the linearization given: Ad [N,6,6], Bd [N,6,2], g [N,6]; xinit [N+1,6] starting
+    states (default zeros).  Returns dict(status, U_opt (2,N), X_opt (6,N+1), objective, iters)."""
+    N = c.N
+    U = np.full((2, N), np.nan)
+    X = np.full((6, N + 1), np.nan)
+    info = OrcInfo()
+    xi = None if xinit is None else _f64(xinit, (N + 1, 6))
+    lib().orc_qp_ipm(C.byref(c), _dp(_f64(x0, 6)), _dp(_f64(u_prev, 2)), _dp(_f64(path_ref, (N + 1, 3))),
+                     _dp(_f64(vref, N + 1)), _dp(_f64(Ad, (N, 6, 6))), _dp(_f64(Bd, (N, 6, 2))), _dp(_f64(g, (N, 6))),
+                     _dp(xi), _dp(U), _dp(X), C.byref(info))
+    return dict(status=info.status, U_opt=U, X_opt=X, objective=info.objective, iters=info.iters,
+                prim_res=info.prim_res, dual_res=info.dual_res)
 
 
 # --------------------------------------------------------------- closed loop helpers

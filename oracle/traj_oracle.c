@@ -52,6 +52,7 @@ void orc_default_cfg(orc_mpc_cfg* c, int N, double Ts) {
     c->polish = 1; c->polish_refine_iter = 3; c->adaptive_rho = 1; c->adaptive_rho_tol = 5.0;
     c->polish_mode = 0; c->polish_max_pass = 8; c->cert_tol = 1e-9; c->polish_max_rounds = 2;
     c->warm_start = 0;
+    c->solver = 1; c->ipm_max_iter = 50; c->ipm_tol = 1e-10;
 }
 
 /* ----------------------------------------------------------------- physics */
@@ -917,6 +918,52 @@ int orc_mpc_step(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], 
     return orc_mpc_step_warm(p, c, x0, u_prev, path_ref, vref, u_cmd, X_opt, U_opt, info, NULL);
 }
 
+/* The QP half by the structured IPM (riccati_ipm.c) on the sparse form, linearization given. */
+int orc_qp_ipm(const orc_mpc_cfg* c, const double x0[6], const double u_prev[2], const double* path_ref,
+               const double* vref, const double* Ad, const double* Bd, const double* gd, const double* xinit,
+               double* U_opt, double* X_opt, orc_info* info) {
+    const int N = c->N;
+    orc_info dummy;
+    if (!info) info = &dummy;
+    memset(info, 0, sizeof(*info));
+    info->polished = -1;
+    info->objective = NAN;
+    if (!all_finite(x0, 6) || !all_finite(u_prev, 2) || !all_finite(path_ref, 3 * (N + 1)) ||
+        !all_finite(vref, N + 1) || !all_finite(Ad, 36 * N) || !all_finite(Bd, 12 * N) || !all_finite(gd, 6 * N)) {
+        info->status = ORC_SOLVER_ERROR;
+        return info->status;
+    }
+    if (!box_rate_feasible(c, u_prev)) {
+        info->status = ORC_INFEASIBLE;
+        return info->status;
+    }
+    double* Q = malloc(sizeof(double) * 36 * (N + 1));
+    double* qv = malloc(sizeof(double) * 6 * (N + 1));
+    double* X = malloc(sizeof(double) * 6 * (N + 1));
+    double* U = malloc(sizeof(double) * 2 * N);
+    double res[5];
+    orc_ipm_state_cost(c, path_ref, vref, Q, qv);
+    int it = 0;
+    const int st = orc_ipm_core(c, N, x0, u_prev, Q, qv, Ad, Bd, gd, xinit, X, U, &it, res);
+    info->status = st;
+    info->iters = it;
+    info->prim_res = res[0] > res[1] ? res[0] : res[1];
+    info->dual_res = res[2];
+    if (st == ORC_OPTIMAL || st == ORC_OPTIMAL_INACCURATE) {
+        double* Xr = malloc(sizeof(double) * 6 * (N + 1));
+        double* Ur = malloc(sizeof(double) * 2 * N);
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < 6; ++i) Xr[i * (N + 1) + k] = X[6 * k + i];
+        for (int k = 0; k < N; ++k) { Ur[k] = U[2 * k]; Ur[N + k] = U[2 * k + 1]; }
+        info->objective = eval_cost(c, x0, u_prev, path_ref, vref, Xr, Ur);
+        if (X_opt) memcpy(X_opt, Xr, sizeof(double) * 6 * (N + 1));
+        if (U_opt) memcpy(U_opt, Ur, sizeof(double) * 2 * N);
+        free(Xr); free(Ur);
+    }
+    free(Q); free(qv); free(X); free(U);
+    return st;
+}
+
 int orc_mpc_step_warm(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], const double u_prev[2],
                       const double* path_ref, const double* vref, double u_cmd[2], double* X_opt, double* U_opt,
                       orc_info* info, orc_warm* warm) {
@@ -930,6 +977,27 @@ int orc_mpc_step_warm(const orc_params* p, const orc_mpc_cfg* c, const double x0
         info->status = ORC_SOLVER_ERROR;
         return info->status;
     }
+    if (c->solver == 2 || (c->solver == 0 && N >= ORC_IPM_AUTO_MIN_N)) {
+        /* structured IPM on the sparse form: nominal rollout + linearization (:165-178), then the QP */
+        double* xbar = malloc(sizeof(double) * 6 * (N + 1));
+        double* xin = malloc(sizeof(double) * 6 * (N + 1));
+        double *Ad = malloc(sizeof(double) * 36 * N), *Bd = malloc(sizeof(double) * 12 * N),
+               *gd = malloc(sizeof(double) * 6 * N);
+        orc_nominal_rollout(p, x0, u_prev, N, c->Ts, xbar);
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < 6; ++i) xin[6 * k + i] = xbar[i * (N + 1) + k];
+        for (int k = 0; k < N; ++k)
+            orc_linearize_discretize(p, xin + 6 * k, u_prev, c->Ts, Ad + 36 * k, Bd + 12 * k, gd + 6 * k);
+        double* U = malloc(sizeof(double) * 2 * N);
+        const int st = orc_qp_ipm(c, x0, u_prev, path_ref, vref, Ad, Bd, gd, xin, U, X_opt, info);
+        if (st == ORC_OPTIMAL || st == ORC_OPTIMAL_INACCURATE) {
+            u_cmd[0] = U[0]; u_cmd[1] = U[N];
+            if (U_opt) memcpy(U_opt, U, sizeof(double) * 2 * N);
+        }
+        if (warm) warm->valid = 0;
+        free(xbar); free(xin); free(Ad); free(Bd); free(gd); free(U);
+        return st;
+    }
     qp_t qp;
     build_qp(p, c, x0, u_prev, path_ref, vref, &qp);
     int st;
@@ -942,6 +1010,25 @@ int orc_mpc_step_warm(const orc_params* p, const orc_mpc_cfg* c, const double x0
         st = osqp_solve(&qp, c, u, info, warm);
     }
     info->status = st;
+    if ((c->solver == 0 || c->solver == 3) && (st == ORC_SOLVER_ERROR || st == ORC_USER_LIMIT)) {
+        /* the condensed problem failed numerically (non-finite condensed data, a failed KKT
+         * factorization, no convergence): solve the sparse form by the structured IPM instead */
+        double* xbar = malloc(sizeof(double) * 6 * (N + 1));
+        double* xin = malloc(sizeof(double) * 6 * (N + 1));
+        double* U = malloc(sizeof(double) * 2 * N);
+        orc_nominal_rollout(p, x0, u_prev, N, c->Ts, xbar);
+        for (int k = 0; k <= N; ++k)
+            for (int i = 0; i < 6; ++i) xin[6 * k + i] = xbar[i * (N + 1) + k];
+        st = orc_qp_ipm(c, x0, u_prev, path_ref, vref, qp.Ad, qp.Bd, qp.gd, xin, U, X_opt, info);
+        if (st == ORC_OPTIMAL || st == ORC_OPTIMAL_INACCURATE) {
+            u_cmd[0] = U[0]; u_cmd[1] = U[N];
+            if (U_opt) memcpy(U_opt, U, sizeof(double) * 2 * N);
+        }
+        if (warm) warm->valid = 0;
+        free(xbar); free(xin); free(U); free(u);
+        qp_free(&qp);
+        return st;
+    }
     if (warm && st != ORC_OPTIMAL && st != ORC_OPTIMAL_INACCURATE) warm->valid = 0;
     if (st == ORC_OPTIMAL || st == ORC_OPTIMAL_INACCURATE) {
         double* X = malloc(sizeof(double) * 6 * (N + 1));

@@ -63,7 +63,17 @@ typedef struct {
     double cert_tol;
     int polish_max_rounds;   /* exact mode: ADMM continuation rounds (tolerance x 1e-2 each) */
     int warm_start;          /* closed loop: start ADMM from the previous step's rho (orc_warm) */
+    /* QP solver (include/trajmpc.h traj_mpc_config.solver): 0 auto -- the condensed ADMM for
+     * N < ORC_IPM_AUTO_MIN_N, falling back to the structured IPM (riccati_ipm.c, sparse form) when it
+     * fails numerically (non-finite condensed data, failed factorization, max_iter), the structured
+     * IPM for longer horizons; 1 condensed ADMM only; 2 structured IPM only; 3 condensed ADMM + IPM
+     * fallback at any N */
+    int solver;
+    int ipm_max_iter;
+    double ipm_tol;          /* relative KKT residual the IPM stops at */
 } orc_mpc_cfg;
+
+#define ORC_IPM_AUTO_MIN_N 33
 
 /* status codes (identical numbering to include/trajmpc.h) */
 enum {
@@ -128,6 +138,20 @@ void orc_mpc_step_batch(const orc_params* p, const orc_mpc_cfg* c, int B, const 
  * box+rate rows only).  Returns 0 on success. U_opt (2,N) row-major. */
 int orc_qp_exact(const orc_params* p, const orc_mpc_cfg* c, const double x0[6], const double u_prev[2],
                  const double* path_ref, const double* vref, double* U_opt, double* objective);
+
+/* ---- structured interior-point solve of the sparse-form QP (riccati_ipm.c) ----
+ * Q [N+1,36] / qv [N+1,6]: state cost per stage (orc_ipm_state_cost); Ad/Bd/gd the linearization
+ * ([N,36], [N,12], [N,6]); xinit [N+1,6] starting states or NULL.  Outputs X [N+1,6], U [N,2] (stage-
+ * major), iterations, residuals (dynamics, rows, stationarity, mu, gradient scale).  Returns a status. */
+int orc_ipm_core(const orc_mpc_cfg* c, int N, const double* x0, const double* u_prev, const double* Q,
+                 const double* qv, const double* Ad, const double* Bd, const double* gd, const double* xinit,
+                 double* X, double* U, int* iters, double* res);
+void orc_ipm_state_cost(const orc_mpc_cfg* c, const double* path_ref, const double* vref, double* Q, double* qv);
+/* The QP half (mpc_6stati.py:180-275) by the structured IPM with the linearization given (Ad [N,6,6],
+ * Bd [N,6,2], gd [N,6]); U_opt (2,N), X_opt (6,N+1) row-major (may be NULL); info->polished = -1. */
+int orc_qp_ipm(const orc_mpc_cfg* c, const double x0[6], const double u_prev[2], const double* path_ref,
+               const double* vref, const double* Ad, const double* Bd, const double* gd, const double* xinit,
+               double* U_opt, double* X_opt, orc_info* info);
 
 /* ---- closed-loop caller (MPC/main.py) ---- */
 double orc_d_steady_state(const orc_params* p, double v);

@@ -116,3 +116,64 @@ def test_infeasible_and_nonfinite(oracle_lib):
     pr2 = pr.copy(); pr2[3, 1] = np.nan
     r = O.mpc_step(x0, [0.1, 0.0], pr2, v, c)
     assert r["status"] == 6 and np.allclose(r["u_cmd"], [0.1, 0.0])
+
+
+@pytest.mark.parametrize("f", QP_FILES)
+def test_sparse_structured_ipm_vs_golden(oracle_lib, f):
+    """Sparse-form QP (X and U as variables, dynamics as equalities -- the form the reference hands to
+    CVXPY, mpc_6stati.py:180-250) solved by the oracle's Riccati-factorized interior point method
+    (oracle/riccati_ipm.c) from the reference's own A, B, g: the same unique optimum as the golden."""
+    O = oracle_lib
+    g = _load(f)
+    N, Ts = int(g["N"]), float(g["Ts"])
+    c = O.cfg(N=N, Ts=Ts, ipm_tol=1e-12, ipm_max_iter=100)
+    for i in range(len(g["x0"])):
+        r = O.qp_ipm(g["x0"][i], g["u_prev"][i], g["path_ref"][i], g["vref"][i], g["Ad"][i], g["Bd"][i],
+                     g["g"][i], c)
+        assert r["status"] == 0 and r["iters"] <= 20
+        # interior point: U converges like sqrt(mu) on degenerate active sets -> 1e-4 abs
+        assert np.abs(r["U_opt"] - g["U_opt"][i]).max() <= 1e-4
+        assert abs(r["objective"] - g["objective"][i]) <= 1e-7 * abs(g["objective"][i])
+
+
+def test_config3_failures_are_reference_rollout_blowups(oracle_lib):
+    """Config 3 (N=40, dt=0.05): every closed-loop step the condensed solver fails on has a REFERENCE
+    nominal rollout (mpc_6stati.py:165-172, recorded from the reference's own f_cont by
+    tests/golden/gen_hard_qp.py) that reaches |x_bar| >= 1e17 or overflows, so the reference's own QP
+    data are non-finite or astronomically scaled there; the oracle's rollout agrees on that, and the
+    oracle's condensed solver reproduces the recorded statuses at those states."""
+    O = oracle_lib
+    g = _load("qp_N40_Ts005_hard")
+    N, Ts = int(g["N"]), float(g["Ts"])
+    fail = g["failing"] == 1
+    assert fail.sum() >= 30 and (~fail).sum() >= 32
+    assert float(g["run_fail_min_xbar"]) >= 1e15                  # whole run, not only the kept rows
+    assert np.all(g["ref_xbar_max"][fail] >= 1e15)
+    assert np.all(g["condensed_status"][fail] >= 2) and np.all(g["condensed_status"][~fail] <= 1)
+    c = O.cfg(N=N, Ts=Ts)
+    for i in range(len(g["x0"])):
+        if not np.isfinite(g["x0"][i]).all():
+            continue
+        xb = O.nominal_rollout(g["x0"][i], g["u_prev"][i], N, Ts)
+        m = np.abs(xb).max() if np.isfinite(xb).all() else np.inf
+        # both rollouts are the same float64 recurrence: finite together, and the same order of magnitude
+        assert np.isfinite(m) == np.isfinite(g["ref_xbar_max"][i])
+        if np.isfinite(m):
+            assert abs(np.log10(m) - np.log10(g["ref_xbar_max"][i])) < 1.0
+        r = O.mpc_step(g["x0"][i], g["u_prev"][i], g["path_ref"][i], g["vref"][i], c)
+        assert r["status"] == g["condensed_status"][i]
+        if fail[i]:
+            assert np.array_equal(r["u_cmd"], g["u_prev"][i])     # mpc_6stati.py:257-262 fallback
+    # controls: where the condensed solver's exact mode CERTIFIES its point (KKT at 1e-9), it and the
+    # sparse form (IPM) reach the same optimum.  Uncertified ADMM points (OSQP's polish accepts by a
+    # residual comparison) can be far from it at this conditioning: DESIGN.md "Config 3".
+    ok = (~fail) & (g["ipm_status"] == 0) & (g["ref_xbar_max"] < 1e3)
+    assert ok.sum() >= 32
+    cx = O.cfg(N=N, Ts=Ts, polish_mode=1)
+    ncert = 0
+    for i in np.where(ok)[0]:
+        r = O.mpc_step(g["x0"][i], g["u_prev"][i], g["path_ref"][i], g["vref"][i], cx)
+        if r["polished"] > 0:
+            ncert += 1
+            assert np.abs(r["u_cmd"] - g["U_opt"][i][:, 0]).max() <= 1e-4
+    assert ncert >= 16
