@@ -10,7 +10,8 @@ HBM for the whole timed region.  The roofline object is solve_kernel's (the domi
 timed with HIP events the library records on the launch stream.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 20] [--dt 0.05]
-  N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ...
+  N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 ... --gpus N,
+         or plain `python bench.py --gpus N`, which starts the N worker processes itself (RCCL)
 
 Multi-GPU: trajectories are independent, so each rank owns its own B trajectories (ids
 rank*B .. rank*B+B-1, weak scaling) with no data-path collective; the ranks only meet at the
@@ -178,6 +179,73 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
     return out
 
 
+def _spawn_workers(n):
+    """bench.py --gpus N without a launcher: N worker processes (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous
+    on 127.0.0.1), each runs this script on its own GPU over RCCL; the parent never touches the GPU and
+    exits with the first non-zero worker status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        sys.exit(bad[0])
+
+
+def dataset_leg(args, w, dev, dist, rank, world):
+    """BASELINE.json configs[3] on this node: every rank runs the closed loop of its --batch trajectories
+    (ids rank * B + i, the bench workload) for --dataset-steps steps from the initial states, the packed
+    [B, T+1, 9] histories go to rank 0 with one dist.gather (RCCL over xGMI), and rank 0 optionally
+    writes the CSVs.  Generation, gather and CSV writing are timed separately (max over ranks)."""
+    from trajectory_generation_amd import dataset as D
+    B, N, Ts, T = args.batch, args.horizon, args.dt, args.dataset_steps
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=dev)
+    cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=args.polish_mode)
+
+    def bar():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    bar()
+    t0 = time.perf_counter()
+    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg)
+    blk = D.pack_history(res["X"], res["U"], res["status"])
+    bar()
+    t1 = time.perf_counter()
+    full = D.gather_to_root(blk, dist)
+    bar()
+    t2 = time.perf_counter()
+    times = torch.tensor([t1 - t0, t2 - t1], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+    gen_s, gather_s = (float(v) for v in times.cpu())
+    if rank != 0:
+        return None
+    X, U, st = D.unpack_history(full)
+    csv_s = None
+    if args.dataset_csv:
+        os.makedirs(args.dataset_csv, exist_ok=True)
+        t3 = time.perf_counter()
+        D.write_csv(os.path.join(args.dataset_csv, "vehicle_mpc"), X.cpu().numpy(), U.cpu().numpy(),
+                    np.arange(X.shape[0]), Ts)
+        csv_s = time.perf_counter() - t3
+    n = world * B * T
+    return {"what": "configs[3]: closed-loop dataset generation, histories gathered into rank 0",
+            "trajectories": world * B, "steps": T, "traj_steps_per_s": n / gen_s, "generate_s": gen_s,
+            "gather_s": gather_s, "gather_bytes": int(full.numel() * full.element_size()),
+            "csv_s": csv_s, "status_hist": torch.bincount(st.reshape(-1).long(), minlength=7).tolist()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -194,22 +262,35 @@ def main():
     ap.add_argument("--no-knet", action="store_true", help="skip the KalmanNet measurement (configs[4])")
     ap.add_argument("--per-step", action="store_true",
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r01.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r02.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
-    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r01.json"),
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r02.json"),
                     help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
     ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r01.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
+    ap.add_argument("--dataset-steps", type=int, default=240,
+                    help="configs[3] leg: closed-loop dataset generation of --batch trajectories per GPU over this "
+                         "many steps, then the histories gathered into rank 0 (0 disables)")
+    ap.add_argument("--dataset-csv", default=None,
+                    help="directory: rank 0 also writes the dataset CSVs there (timed separately)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: start one worker process per GPU before anything in this process touches the GPU
+        return _spawn_workers(args.gpus)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus and args.gpus != 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    world = 1
+    if world_env > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        world = dist.get_world_size()
+        assert world == world_env
     dev = TB.require_gpu(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -270,6 +351,7 @@ def main():
     steps_per_launch = args.steps if fused else 1
     iters = it[args.warmup:].cpu().numpy().reshape(-1)
     stat = st[args.warmup:].cpu().numpy().reshape(-1)
+    dataset = dataset_leg(args, w, dev, dist, rank, world) if args.dataset_steps > 0 else None
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -285,8 +367,12 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("batch") == B and tj.get("horizon") == N:
-                if bool(tj.get("fused", False)) == fused and int(tj.get("steps_per_launch", 1)) == steps_per_launch:
+            if tj.get("horizon") == N and bool(tj.get("fused", False)) == fused:
+                if fused and tj.get("hbm_bytes_per_instance_step"):
+                    # PMC bytes per instance-step of the profiled fused launch x this launch's instance-steps
+                    traffic = float(tj["hbm_bytes_per_instance_step"]) * B * steps_per_launch
+                    traffic_step = float(tj["hbm_bytes_per_instance_step"]) * B
+                elif tj.get("batch") == B and int(tj.get("steps_per_launch", 1)) == steps_per_launch:
                     traffic = tj.get("hbm_bytes_per_kernel", {}).get("solve_kernel")
                     traffic_step = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
@@ -331,12 +417,13 @@ def main():
                          f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
                      "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
                      "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,
-                     "traffic_source": os.path.relpath(args.traffic_json, HERE) if traffic is not None else None,
+                     "traffic_source": os.path.relpath(os.path.abspath(args.traffic_json), HERE) if traffic is not None else None,
                      "issue": issue},
         "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
                          "iters_max": int(iters.max()),
                          "status_hist": np.bincount(stat, minlength=7).tolist()},
     }
+    out["dataset"] = dataset
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(w, N, Ts, min(args.cpu_traj, B), args.cpu_steps, args.polish_mode,
                                            cfg.warm_start)

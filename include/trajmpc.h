@@ -51,6 +51,7 @@ extern "C" {
 #define TRAJ_E_ARG (-1)          /* bad argument (null pointer, B < 0, N out of range, ...) */
 #define TRAJ_E_UNSUPPORTED (-2)  /* configuration this build does not implement */
 #define TRAJ_E_LAUNCH (-3)       /* HIP launch failure */
+#define TRAJ_E_HANDOFF (-4)      /* traj_closed_loop_check: a fused-run instance hand-off timed out */
 
 /* per-instance status codes: CVXPY strings in brackets (mpc_6stati.py:257-262) */
 #define TRAJ_STATUS_OPTIMAL 0                /* "optimal" */
@@ -180,6 +181,14 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
                          double* hist_x, double* hist_u, int* status, int* iters, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+/* Synchronizes `stream` and reports whether the last traj_closed_loop_run on this workspace lost an
+ * instance hand-off: a workgroup that waited for an instance's previous step longer than the spin
+ * bound (traj_debug_spin_limit) went on with the state it found, so the run's x / u_prev / history
+ * are not the closed loop's -- TRAJ_E_HANDOFF, never TRAJ_OK, in that case.  Call it after every
+ * traj_closed_loop_run (the Python wrapper batch.closed_loop_run does) and before the next run on the
+ * same workspace (a run clears the flag when it starts). */
+int traj_closed_loop_check(const void* workspace, size_t workspace_bytes, int B, int N, void* stream);
+
 /* ---- diagnostics ----
  * Subsequent MPC launches write, per instance b, 32 int64 slots at buf[32 b ..] (device memory):
  * [0..7] s_memtime at phase boundaries (start, inputs, rollout, linearization, condensing,
@@ -188,6 +197,10 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
  * [16..19] s_memtime inside the condensing phase (staging issued, staging landed, stage loop, P rows).
  * NULL disables.  For profiling only; never enabled by the product path. */
 int traj_debug_set_stamps(long long* buf);
+/* Subsequent traj_closed_loop_run launches write, per work item q = step * B + rank, 4 int64 at
+ * buf[4 q ..] (device memory, [steps * B, 4]): drawn from the queue, previous step seen (wait over),
+ * step done (s_memrealtime, 100 MHz), workgroup.  NULL disables.  Diagnostics only. */
+int traj_debug_set_item_stamps(long long* buf);
 
 /* Per-kernel timing of the next max_steps traj_closed_loop_step calls: HIP events recorded on the
  * launch stream around rollout_kernel, jac_kernel, order_kernel and solve_kernel (0 frees them).
@@ -197,6 +210,9 @@ int traj_debug_kernel_timing(int max_steps);
 /* traj_closed_loop_run's grid: the resident workgroup slots of the device (0, default) or the given
  * count (at least ceil(B / 8)); each workgroup runs its instances step by step.  For tests. */
 int traj_debug_fused_grid(int workgroups);
+/* Polls of an instance's step counter before a fused-run hand-off is declared lost (0: the default,
+ * 2^22 polls with s_sleep back-off, seconds).  For the test that the loss is reported. */
+int traj_debug_spin_limit(int polls);
 int traj_debug_kernel_times(double* ms, int* n_steps);
 
 #ifdef __cplusplus

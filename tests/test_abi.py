@@ -172,3 +172,29 @@ def test_product_path_has_no_oracle_dependency():
                 assert not re.search(r"^\s*(import|from)\s+oracle\b|traj_oracle|pyoracle", src, flags=re.M), f
     out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
     assert "traj_oracle" not in out
+
+
+def test_bench_spawns_one_worker_per_gpu(monkeypatch):
+    """`bench.py --gpus N` without a launcher starts N worker processes (RANK / LOCAL_RANK / WORLD_SIZE,
+    rendezvous on 127.0.0.1) from a parent that never touches the GPU, and fails when a worker fails."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    started = []
+
+    class P:
+        def __init__(self, cmd, env):
+            started.append((cmd, env))
+
+        def wait(self):
+            return 0 if started[-1][1]["RANK"] != "9" else 3
+
+    monkeypatch.setattr(subprocess, "Popen", P)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    bench._spawn_workers(4)
+    assert [e["RANK"] for _, e in started] == ["0", "1", "2", "3"]
+    assert all(e["WORLD_SIZE"] == "4" and e["LOCAL_RANK"] == e["RANK"] and e["MASTER_ADDR"] == "127.0.0.1"
+               for _, e in started)
+    assert all(c[-4:] == ["--gpus", "4", "--steps", "3"] and c[1].endswith("bench.py") for c, _ in started)
+    assert "torch.cuda" not in sys.modules or not __import__("torch").cuda.is_initialized()

@@ -47,49 +47,70 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _fake_closed_loop(w, T, cfg):
+    """CPU stand-in for one rank's closed loop: histories that encode the trajectory id and the step."""
+    ids = np.asarray(w["ids"], dtype=np.float64)
+    B = len(ids)
+    X = torch.tensor(ids[:, None, None] + 0.01 * np.arange(T + 1)[None, :, None] + w["x0"][:, None, :] * 0.0)
+    X[:, 0] = torch.tensor(w["x0"])
+    U = torch.tensor(-ids[:, None, None] + np.zeros((1, T, 2)))
+    st = torch.tensor((ids[None, :].astype(np.int64) + np.arange(T)[:, None]) % 7, dtype=torch.int32)
+    return dict(X=X, U=U, status=st)
+
+
+def _worker(rank, world, port, q, out_prefix):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     B, T = 4, 6
-    ids = np.arange(rank * B, rank * B + B)
-    X = torch.tensor(ids[:, None, None] + 0.01 * np.arange(T + 1)[None, :, None] + np.zeros((1, 1, 6)))
-    U = torch.tensor(-ids[:, None, None] + np.zeros((1, T, 2)))
-    gX, gU = D.gather_histories(X, U, dist)
+    r = D.generate(B, T, N=20, Ts=0.05, kind="spline", seed=3, out_prefix=out_prefix, dist=dist,
+                   closed_loop=_fake_closed_loop)
     if rank == 0:
-        q.put((gX.numpy(), gU.numpy()))
+        X, U, st = r
+        q.put((X.numpy(), U.numpy(), st.numpy()))
+    else:
+        q.put(r)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gather_two_ranks_gloo():
+def test_generate_two_ranks_gloo(tmp_path):
+    """dataset.generate at world size 2 (gloo): rank r runs ids [r B, (r+1) B) (the workload's own id
+    offset, merge_datasets.py:41-47 semantics), the packed histories and statuses reach rank 0 only,
+    in id order, and rank 0 writes the CSVs with the global trajectory ids."""
+    from trajectory_generation_amd.workload import make_workload
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    prefix = str(tmp_path / "ds")
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, prefix)) for r in range(2)]
     for p in procs:
         p.start()
-    gX, gU = q.get(timeout=120)
+    got = [q.get(timeout=120) for _ in range(2)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert gX.shape == (8, 7, 6) and gU.shape == (8, 6, 2)
-    np.testing.assert_array_equal(gX[:, 0, 0], np.arange(8))      # rank order == global id order
+    assert sum(g is None for g in got) == 1          # rank 1 receives nothing
+    gX, gU, st = next(g for g in got if g is not None)
+    assert gX.shape == (8, 7, 6) and gU.shape == (8, 6, 2) and st.shape == (6, 8)
+    np.testing.assert_array_equal(gX[:, 1, 0], np.arange(8) + 0.01)   # rank order == global id order
     np.testing.assert_array_equal(gU[:, 0, 0], -np.arange(8))
+    np.testing.assert_array_equal(st, (np.arange(8)[None, :] + np.arange(6)[:, None]) % 7)
+    # step 0 = each id's own initial state: rank 1's share is ids 4..7 of the same seeded workload
+    w = make_workload(8, 20, 0.05, kind="spline", seed=3)
+    np.testing.assert_array_equal(gX[:, 0, :], w["x0"])
+    import pandas as pd
+    clean = pd.read_csv(prefix + "_clean.csv")
+    noisy = pd.read_csv(prefix + "_noisy.csv")
+    assert sorted(clean["trajectory_id"].unique()) == list(range(8))
+    assert len(clean) == 8 * 7 and len(noisy) == 8 * 7
+    np.testing.assert_allclose(clean["X"].to_numpy().reshape(8, 7), gX[:, :, 0], rtol=0, atol=1e-12)
 
 
-def test_loader_matches_reference(tmp_path):
-    """dataset.load_vehicle_dataset vs the reference's data_loader.py on the same CSVs (tests/golden/loader.npz)."""
-    import sys
-    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
-    from gen_loader_golden import synthetic_histories
-    X, U, Ts = synthetic_histories()
-    clean, noisy = D.frames(X, U, np.arange(X.shape[0]), Ts)
-    clean.to_csv(tmp_path / "c.csv", index=False)
-    noisy.to_csv(tmp_path / "n.csv", index=False)
-    got = D.load_vehicle_dataset(tmp_path / "n.csv", tmp_path / "c.csv", T_steps=25)
-    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "loader.npz"))
-    for name, part in zip(("train", "val", "test"), got):
-        for k, t in zip("yux", part):
-            np.testing.assert_array_equal(t.numpy(), g[f"{name}_{k}"])
-    assert D.load_vehicle_dataset(tmp_path / "missing.csv", tmp_path / "c.csv") is None
+def test_pack_unpack_history():
+    B, T = 3, 5
+    X = torch.randn(B, T + 1, 6, dtype=torch.float64)
+    U = torch.randn(B, T, 2, dtype=torch.float64)
+    st = torch.randint(0, 7, (T, B), dtype=torch.int32)
+    X2, U2, st2 = D.unpack_history(D.pack_history(X, U, st))
+    assert torch.equal(X2, X) and torch.equal(U2, U) and torch.equal(st2, st)

@@ -384,6 +384,27 @@ def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
         assert torch.equal(per[k], fus2[k]), k
 
 
+def test_fused_lost_handoff_is_an_error(gpu):
+    """A fused-run workgroup that gives up waiting for an instance's previous step (spin bound, here one
+    poll: step 1 items are drawn while step 0 still runs) makes the run an error (TRAJ_E_HANDOFF via
+    traj_closed_loop_check), never TRAJ_OK with stale state; the default bound runs clean afterwards."""
+    from trajectory_generation_amd import _lib
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B = 20, 0.05, 6, 16
+    w = make_workload(B, N, Ts, kind="spline", seed=3)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts)
+    try:
+        _lib.check(_lib.lib().traj_debug_spin_limit(1), "traj_debug_spin_limit")
+        with pytest.raises(RuntimeError, match="hand-off"):
+            TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    finally:
+        _lib.lib().traj_debug_spin_limit(0)
+    ok = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    assert torch.equal(ok["X"], per["X"])
+
+
 # ------------------------------------------------------------------ drop-in module
 
 def test_dropin_mpc_step_contract(gpu, oracle_lib):
@@ -499,18 +520,23 @@ def test_state_bounds_edge_cases(gpu, oracle_lib):
 
 # ------------------------------------------------------------------ dataset emitter (f1)
 
-def test_dataset_generate_single_rank(gpu, tmp_path):
+def test_dataset_generate_single_rank(gpu, oracle_lib, tmp_path):
+    """dataset.generate (GPU closed loop -> packed history -> CSV) against the C oracle's closed loop of
+    the same workload (Ts = 0.02: the stable regime where whole trajectories agree), and the CSVs
+    against the histories it returns."""
     import pandas as pd
     from trajectory_generation_amd import dataset as D
     from trajectory_generation_amd.workload import make_workload
-    B, T, N, Ts = 6, 8, 20, 0.05
+    B, T, N, Ts = 6, 30, 20, 0.02
     X, U, st = D.generate(B, T, N=N, Ts=Ts, kind="spline", seed=1, out_prefix=str(tmp_path / "ds"))
     w = make_workload(B, N, Ts, kind="spline", seed=1)
-    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
-    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts))
-    assert torch.equal(X, res["X"]) and torch.equal(U, res["U"])
-    assert st.shape == (B, T)
+    O = oracle_lib
+    r = O.closed_loop_batch(_oracle_paths(O, w), w["x0"], w["u0"], w["vref"], T, O.cfg(N=N, Ts=Ts, warm_start=1))
+    assert np.array_equal(st.cpu().numpy(), r["status"].T)
+    assert np.abs(X.cpu().numpy() - r["X"]).max() <= 1e-3
+    assert st.shape == (T, B)
     clean = pd.read_csv(tmp_path / "ds_clean.csv", float_precision="round_trip")
     noisy = pd.read_csv(tmp_path / "ds_noisy.csv", float_precision="round_trip")
     assert len(clean) == B * (T + 1) and list(noisy.columns)[-1] == "trajectory_id"
     np.testing.assert_allclose(clean["phi"].to_numpy().reshape(B, T + 1), X[:, :, 2].cpu().numpy(), rtol=0, atol=0)
+    np.testing.assert_allclose(clean["d"].to_numpy().reshape(B, T + 1)[:, :T], U[:, :, 0].cpu().numpy(), rtol=0, atol=0)

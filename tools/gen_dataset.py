@@ -5,7 +5,8 @@ node, N = 20, dt = 0.05 s, 240 steps), writing the reference's clean / noisy CSV
   python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
       tools/gen_dataset.py --per-gpu 4096 --steps 240 --out vehicle_mpc
 
-Prints the generation rate (trajectory-steps/s, CSV writing excluded) as JSON on rank 0."""
+Prints the generation rate (trajectory-steps/s incl. the gather into rank 0, CSV writing excluded) as JSON
+on rank 0.  bench.py's dataset leg measures the same with generation and gather timed apart."""
 import argparse
 import json
 import os
@@ -35,17 +36,15 @@ def main():
     from trajectory_generation_amd import dataset as D
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    X, U, st = D.generate(a.per_gpu, a.steps, N=a.horizon, Ts=a.dt, kind=a.kind, out_prefix=None, dist=dist)
+    r = D.generate(a.per_gpu, a.steps, N=a.horizon, Ts=a.dt, kind=a.kind, out_prefix=None, dist=dist)
     torch.cuda.synchronize()
-    t_gen = time.perf_counter() - t0
-    rank = dist.get_rank() if dist else 0
-    if rank == 0:
+    t_gen = time.perf_counter() - t0          # closed loop + gather into rank 0
+    if r is not None:                         # rank 0
+        X, U, st = r
         t1 = time.perf_counter()
         if a.out:
             import numpy as np
-            clean, noisy = D.frames(X.cpu().numpy(), U.cpu().numpy(), np.arange(X.shape[0]), a.dt)
-            clean.to_csv(f"{a.out}_clean.csv", index=False)
-            noisy.to_csv(f"{a.out}_noisy.csv", index=False)
+            D.write_csv(a.out, X.cpu().numpy(), U.cpu().numpy(), np.arange(X.shape[0]), a.dt)
         t_csv = time.perf_counter() - t1
         n = X.shape[0] * a.steps
         print(json.dumps({"trajectories": int(X.shape[0]), "steps": a.steps, "n_gpus": world,

@@ -84,6 +84,7 @@ def main():
                "fetch_bytes_per_launch": {"solve_kernel": fb}, "write_bytes_per_launch": {"solve_kernel": wb},
                "hbm_bytes_per_kernel": {"solve_kernel": fb + wb}, "hbm_bytes_per_launch": fb + wb,
                "hbm_bytes_per_step": (fb + wb) / a.fused_steps,
+               "hbm_bytes_per_instance_step": (fb + wb) / (a.fused_steps * a.batch),
                "note": "fused traj_closed_loop_run launch of fused_steps steps; FETCH_SIZE x2 (gfx950 correction), "
                        "KiB -> bytes"}
         with open(a.out, "w") as f:

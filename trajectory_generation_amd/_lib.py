@@ -16,7 +16,7 @@ CSRC = os.path.join(_HERE, "csrc")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "trajmpc.h")
 HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "trajknet.h")]
 
-TRAJ_OK, TRAJ_E_ARG, TRAJ_E_UNSUPPORTED, TRAJ_E_LAUNCH = 0, -1, -2, -3
+TRAJ_OK, TRAJ_E_ARG, TRAJ_E_UNSUPPORTED, TRAJ_E_LAUNCH, TRAJ_E_HANDOFF = 0, -1, -2, -3, -4
 MAX_N = 40
 
 STATUS_STRINGS = {
@@ -106,6 +106,9 @@ _SIGS = {
     "traj_debug_set_stamps": (C.c_int, [_V]),
     "traj_debug_kernel_timing": (C.c_int, [C.c_int]),
     "traj_debug_fused_grid": (C.c_int, [C.c_int]),
+    "traj_debug_spin_limit": (C.c_int, [C.c_int]),
+    "traj_debug_set_item_stamps": (C.c_int, [_V]),
+    "traj_closed_loop_check": (C.c_int, [_V, C.c_size_t, C.c_int, C.c_int, _V]),
     "traj_debug_kernel_times": (C.c_int, [_V, _V]),
     "traj_knet_prior_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float, C.c_int,
                                       _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),

@@ -312,9 +312,10 @@ def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=Non
 
 
 def closed_loop_run(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None, t0=0, steps=1, hist_x=None,
-                    hist_u=None, status=None, iters=None):
+                    hist_u=None, status=None, iters=None, check=True):
     """Steps t0 .. t0+steps-1 of MPC/main.py:85-101 in ONE fused launch (traj_closed_loop_run), bit-identical
-    to `steps` closed_loop_step calls; x, u_prev updated in place; status / iters [steps, B]."""
+    to `steps` closed_loop_step calls; x, u_prev updated in place; status / iters [steps, B].
+    check: synchronize and raise RuntimeError if the run lost an instance hand-off (traj_closed_loop_check)."""
     B = x.shape[0]
     ps = paths.struct()
     T = hist_u.shape[1] if hist_u is not None else 0
@@ -323,6 +324,9 @@ def closed_loop_run(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None
         C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t0),
         int(steps), int(T), _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()),
         "traj_closed_loop_run")
+    if check:   # synchronizes: a lost instance hand-off raises instead of returning stale trajectories
+        _lib.check(_lib.lib().traj_closed_loop_check(_p(ws), ws.numel() * 8, B, cfg.N, _stream()),
+                   "traj_closed_loop_run")
 
 
 def run_closed_loop(x0, u0, paths: PathSet, vref, T, cfg: MpcConfig, params=None, record=True, fused=True) -> dict:

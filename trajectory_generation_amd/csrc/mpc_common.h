@@ -78,6 +78,8 @@ struct KArgs {
     int nsteps;              // > 0: fused closed loop, nsteps steps per launch (status / iters [nsteps, B])
     int fused_grid;          // fused: workgroups to launch (0: the resident slots; traj_debug_fused_grid)
     int* queue;              // fused: [0] next work item, [1] error flag, [2 + b] completed steps of b
+    int spin_limit;          // fused: polls of a step counter before a hand-off is declared lost
+    long long* dbg_items;    // fused diagnostics: per work item q [4]: drawn, wait over, done (100 MHz), slot
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

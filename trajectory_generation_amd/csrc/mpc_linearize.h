@@ -242,10 +242,9 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 // A_k, B_k, g_k written to LDS in the solve kernel's staging layout.  xs / us: the state and input
 // (LDS); xf: scratch [N][12] (LDS).  Ends with a workgroup barrier.
 template <int NT>
-__device__ __forceinline__ void block_linearize(const VP& p, int N, double Ts, const double* xs, const double* us,
-                                                double* xf, double* A, double* Bm, double* g,
+__device__ __forceinline__ void block_linearize(const int t, const VP& p, int N, double Ts, const double* xs,
+                                                const double* us, double* xf, double* A, double* Bm, double* g,
                                                 long long* dbg = nullptr) {
-    const int t = threadIdx.x;
     auto mark = [&](int i) { if (dbg && t == 0) dbg[i] = __builtin_amdgcn_s_memtime(); };
     if (t < 64) {
         // rollout (rollout_kernel's arithmetic): per stage, lanes 0 / 1 / 2 run the front-tire chain,

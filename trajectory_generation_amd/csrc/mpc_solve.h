@@ -19,6 +19,13 @@
 #include "mpc_common.h"
 #include "mpc_linearize.h"
 
+#ifndef TGMPC_PRIO_ITERS
+#define TGMPC_PRIO_ITERS 100   // fused run: ADMM iterations after which a solve's wave takes issue priority
+#endif
+#ifndef TGMPC_PRIO_RANK
+#define TGMPC_PRIO_RANK 0      // fused run: heaviest ranks (per mille of B) whose items run at priority 2
+#endif
+
 namespace tgmpc {
 
 // Fused closed loop: an instance's state (x, u_prev, warm record) passes between workgroups -- on any XCD
@@ -77,8 +84,17 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // release / acquire on the per-instance step counter, so a slow solve delays only its instance
     // and every slot stays busy until the queue is drained.
     bool more = true;
+    int rank_of_item = 0;   // fused: rank of the current work item within its step (diagnostics)
     for (int step = 0; more; ++step) {
-    const KArgs& a = a0;
+    // fused: the arguments are read through a pointer the compiler cannot see through, so nothing
+    // derived from them (weights, reciprocals, per-stage predicates, address offsets) is hoisted out of
+    // the step loop -- hoisted, those values stay live across the whole solve and spill
+    typedef __attribute__((address_space(4))) const KArgs* KArgsPtr;   // constant (kernarg) space: s_load
+    // (a0 is the kernel's only argument: it sits at offset 0 of the kernarg segment; &a0 would copy it
+    // to private memory)
+    KArgsPtr ap = FUSED ? (KArgsPtr)__builtin_amdgcn_kernarg_segment_ptr() : (KArgsPtr) nullptr;
+    if constexpr (FUSED) asm volatile("" : "+s"(ap));
+    const KArgs& a = FUSED ? *(const KArgs*)ap : a0;
     int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
     if constexpr (FUSED) {
         __syncthreads();
@@ -86,20 +102,33 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         __syncthreads();
         const int q = s_item;
         if (q >= a.B * a.nsteps) break;
+        if (a.dbg_items && threadIdx.x == 0) a.dbg_items[4 * (size_t)q] = __builtin_amdgcn_s_memrealtime();
         step = q / a.B;
         const int rank = q - step * a.B;
+        rank_of_item = rank;
         b = a.perm ? a.perm[rank] : rank;
+        // issue priority (s_setprio): the wave that works on a long chain gets the SIMD first -- see the
+        // ADMM loop; every item starts at the default priority
+        __builtin_amdgcn_s_setprio(0);
+#if TGMPC_PRIO_RANK > 0
+        if (a.perm && rank * 1000 < a.B * TGMPC_PRIO_RANK) __builtin_amdgcn_s_setprio(2);
+#endif
         if (threadIdx.x == 0 && step > 0) {
             int spins = 0;
             while (__hip_atomic_load(&a.queue[2 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < step) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1 << 22)) {   // bounded: a lost hand-off is reported, never a hang
+                if (++spins > a.spin_limit) {   // bounded: a lost hand-off is reported, never a hang
+                    // (traj_closed_loop_run's caller gets TRAJ_E_HANDOFF from traj_closed_loop_check)
                     __hip_atomic_store(&a.queue[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
             }
         }
         __syncthreads();
+        if (a.dbg_items && threadIdx.x == 0) {   // diagnostics: item timeline (traj_debug_set_item_stamps)
+            a.dbg_items[4 * (size_t)q + 1] = __builtin_amdgcn_s_memrealtime();
+            a.dbg_items[4 * (size_t)q + 3] = blockIdx.x;
+        }
         if (a.dbg && threadIdx.x == 0 && step == 0) {   // diagnostics: start, HW_ID, XCC_ID
             unsigned hw, xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
@@ -239,7 +268,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
     if (fused) {
         // s_F (the condensing's F rows) is the rollout record's scratch here; zeroed again after
-        block_linearize<NT>(p, N, Ts, s_x0, s_up, s_F, s_big, s_big + 36 * N, s_big + 48 * N,
+        block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_F, s_big, s_big + 36 * N, s_big + 48 * N,
                             a.dbg ? a.dbg + (size_t)b * 32 : nullptr);
         for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     } else if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
@@ -535,7 +564,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             cw[C_LB * NT] = lb; cw[C_UB * NT] = ub; cw[C_LR * NT] = lr; cw[C_UR * NT] = ur;
             cw[C_ARUP * NT] = a_r_up0;
         }
-        auto cold = [&](int i) -> double { return ((volatile double*)s_cold)[i * NT + t]; };
+        // (an LDS-typed volatile pointer: ds_read with a 32-bit address -- a generic volatile pointer
+        // becomes a flat load with a 64-bit address per value)
+        typedef __attribute__((address_space(3))) volatile double* LdsVD;
+        auto cold = [&](int i) -> double { return ((LdsVD)s_cold)[i * NT + t]; };
         // scaled P to LDS (row stride PS)
         // packed upper triangle: P(i, j), i <= j, at i*NN - i(i-1)/2 + (j - i); rows >= n are zero
         if (t < NN) {
@@ -842,6 +874,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     zr = nzr;
                     if (--chk == 0) {
                         chk = c.check_interval;
+#if TGMPC_PRIO_ITERS > 0
+                        // a long solve is the critical path of its instance's step chain (the fused run
+                        // ends with the slowest chain): its wave issues ahead of the SIMD's other wave
+                        if (FUSED && iter >= TGMPC_PRIO_ITERS) __builtin_amdgcn_s_setprio(3);
+#endif
                         tic();
                         r = residuals(x, zb, zr, yb, yr);
                         toc(cyc_res);
@@ -1088,6 +1125,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     st_coh(m, (step == a.nsteps - 1) ? acc / a.nsteps : acc);
                 }
                 if (step == a.nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // launch span
+                if (a.dbg_items) a.dbg_items[4 * ((size_t)step * a.B + rank_of_item) + 2] = __builtin_amdgcn_s_memrealtime();
                 // hand the instance to whichever workgroup takes its next step: the sc1 state stores
                 // complete (vmcnt(0)), then the step counter is stored sc1 (no L2 writeback)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -227,7 +227,9 @@ static int launch_general(const KArgs& a, hipStream_t st) {
 }
 
 static long long* g_dbg = nullptr;  // diagnostics buffer (traj_debug_set_stamps)
+static long long* g_dbg_items = nullptr;  // fused-run item timeline (traj_debug_set_item_stamps)
 static int g_fused_grid = 0;        // traj_debug_fused_grid
+static int g_spin_limit = 1 << 22;  // traj_debug_spin_limit: polls before a fused hand-off is declared lost
 
 // per-kernel timing of traj_closed_loop_step (traj_debug_kernel_timing): 5 events per step bracket
 // rollout | jac | order | solve on the launch stream
@@ -252,9 +254,20 @@ int traj_debug_set_stamps(long long* buf) {
     return TRAJ_OK;
 }
 
+int traj_debug_set_item_stamps(long long* buf) {
+    g_dbg_items = buf;
+    return TRAJ_OK;
+}
+
 int traj_debug_fused_grid(int workgroups) {
     if (workgroups < 0) return TRAJ_E_ARG;
     g_fused_grid = workgroups;
+    return TRAJ_OK;
+}
+
+int traj_debug_spin_limit(int polls) {
+    if (polls < 0) return TRAJ_E_ARG;
+    g_spin_limit = polls ? polls : (1 << 22);
     return TRAJ_OK;
 }
 
@@ -307,6 +320,7 @@ const char* traj_error_string(int e) {
         case TRAJ_E_ARG: return "invalid argument";
         case TRAJ_E_UNSUPPORTED: return "unsupported configuration";
         case TRAJ_E_LAUNCH: return "HIP launch failure";
+        case TRAJ_E_HANDOFF: return "fused closed loop: an instance hand-off timed out (results invalid)";
         default: return "unknown error";
     }
 }
@@ -530,6 +544,8 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.dbg = g_dbg;
     a.nsteps = steps;
     a.fused_grid = g_fused_grid;
+    a.spin_limit = g_spin_limit;
+    a.dbg_items = g_dbg_items;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
     // step queue: [0] next work item, [1] error flag, [2 + b] steps of instance b completed
@@ -550,6 +566,21 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     stamp(4, st);
     if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
     return e;
+}
+
+int traj_closed_loop_check(const void* workspace, size_t workspace_bytes, int B, int N, void* stream) {
+    if (B < 0 || N < 1 || N > TRAJ_MAX_N) return TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, N)) return TRAJ_E_ARG;
+    KArgs a;
+    std::memset(&a, 0, sizeof(a));
+    carve_workspace(a, const_cast<void*>(workspace), B, N);
+    const int* flag = (const int*)(a.wsWarm + (size_t)B * 4) + B + 1;   // traj_closed_loop_run's queue[1]
+    int h = 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemcpyAsync(&h, flag, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return TRAJ_E_LAUNCH;
+    if (hipStreamSynchronize(st) != hipSuccess) return TRAJ_E_LAUNCH;
+    return h ? TRAJ_E_HANDOFF : TRAJ_OK;
 }
 
 }  // extern "C"

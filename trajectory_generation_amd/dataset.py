@@ -14,7 +14,8 @@ generation_type1.py:19-33, :312-322).  These files feed merge_datasets.py / data
 
 Sharding: rank r owns trajectory ids [r B, (r+1) B) (ids and per-trajectory seeds are global, so the
 result does not depend on the rank count); the only collective is the final gather of the histories
-to rank 0 over RCCL (all_gather of fixed-size per-rank blocks), after which rank 0 writes the CSVs.
+to rank 0 over RCCL (dist.gather of one fixed-size [B,T+1,9] block per rank; the other ranks receive
+nothing), after which rank 0 writes the CSVs.
 """
 from __future__ import annotations
 
@@ -57,44 +58,83 @@ def frames(X, U, ids, Ts):
     return cols(X, True)[CLEAN_COLUMNS], cols(Xn, False)[NOISY_COLUMNS]
 
 
-def gather_histories(X, U, dist=None):
-    """Concatenate the per-rank [B,T+1,6] / [B,T,2] blocks on every rank (rank order = id order)."""
+HIST_CHANNELS = 9   # per row: X, Y, phi, vx, vy, omega, d, delta (NaN on the last row), status (-1 on the last row)
+
+
+def pack_history(X, U, status):
+    """X [B,T+1,6], U [B,T,2], status [T,B] -> one [B,T+1,9] float64 block (the unit of the gather)."""
+    import torch
+    B, T1 = X.shape[0], X.shape[1]
+    blk = torch.empty((B, T1, HIST_CHANNELS), dtype=torch.float64, device=X.device)
+    blk[:, :, 0:6] = X
+    blk[:, :T1 - 1, 6:8] = U
+    blk[:, T1 - 1, 6:8] = float("nan")
+    blk[:, :T1 - 1, 8] = status.t().to(torch.float64)
+    blk[:, T1 - 1, 8] = -1.0
+    return blk
+
+
+def unpack_history(blk):
+    """Inverse of pack_history: (X [B,T+1,6], U [B,T,2], status [T,B] int32)."""
+    import torch
+    return blk[:, :, 0:6], blk[:, :-1, 6:8], blk[:, :-1, 8].t().to(torch.int32)
+
+
+def gather_to_root(blk, dist=None, dst=0):
+    """The dataset's one collective: every rank's fixed-size [B,T+1,9] block goes to
+    rank `dst` only (dist.gather -- RCCL over xGMI with the nccl backend, gloo on CPU).  Returns the
+    concatenation in rank order (= global trajectory-id order, ids are rank * B + i) on `dst`, None on
+    the other ranks; the block itself without a process group."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
-        return X, U
+        return blk
     import torch
-    W = dist.get_world_size()
-    outX = torch.empty((W * X.shape[0],) + tuple(X.shape[1:]), dtype=X.dtype, device=X.device)
-    outU = torch.empty((W * U.shape[0],) + tuple(U.shape[1:]), dtype=U.dtype, device=U.device)
-    dist.all_gather_into_tensor(outX, X.contiguous())
-    dist.all_gather_into_tensor(outU, U.contiguous())
-    return outX, outU
+    blk = blk.contiguous()
+    if dist.get_rank() == dst:
+        parts = [torch.empty_like(blk) for _ in range(dist.get_world_size())]
+        dist.gather(blk, gather_list=parts, dst=dst)
+        return torch.cat(parts, 0)
+    dist.gather(blk, dst=dst)
+    return None
 
 
-def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=None, polish_mode=0):
-    """Run the closed loop for this rank's B trajectories, gather to every rank and (rank 0) write
-    ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv``.  Returns (X, U, status) for all ranks."""
-    import torch
+def _closed_loop_gpu(w, T, cfg):
+    """This rank's closed loop on the GPU (batch.run_closed_loop, fused launch)."""
     from . import batch as TB
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    return TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg)
+
+
+def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=None, polish_mode=0,
+             closed_loop=None):
+    """Run the closed loop for this rank's B trajectories (ids rank * B .. rank * B + B - 1), gather the
+    histories to rank 0 and (rank 0) write ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv``.
+
+    closed_loop(workload, T, cfg) -> dict(X, U, status) runs one rank's share (default: the fused GPU
+    closed loop); tests inject a CPU stand-in to exercise the id offsets and the gather.
+    Returns (X [W B,T+1,6], U [W B,T,2], status [T,W B]) on rank 0 and None on the other ranks."""
     from .workload import make_workload
     rank = dist.get_rank() if (dist is not None and dist.is_initialized()) else 0
     w = make_workload(B, N, Ts, kind=kind, seed=seed, id_offset=rank * B)
-    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
-    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode))
-    X, U = gather_histories(res["X"], res["U"], dist)
-    st = res["status"]
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        allst = torch.empty((dist.get_world_size() * st.shape[0],) + tuple(st.shape[1:]), dtype=st.dtype,
-                            device=st.device)
-        dist.all_gather_into_tensor(allst, st.t().contiguous())
-        st = allst
-    else:
-        st = st.t()
-    if out_prefix is not None and rank == 0:
-        ids = np.arange(X.shape[0])
-        clean, noisy = frames(X.cpu().numpy(), U.cpu().numpy(), ids, Ts)
-        clean.to_csv(f"{out_prefix}_clean.csv", index=False)
-        noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
+    cfg = None
+    if closed_loop is None:
+        from . import batch as TB
+        cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
+        closed_loop = _closed_loop_gpu
+    res = closed_loop(w, T, cfg)
+    blk = gather_to_root(pack_history(res["X"], res["U"], res["status"]), dist)
+    if blk is None:
+        return None
+    X, U, st = unpack_history(blk)
+    if out_prefix is not None:
+        write_csv(out_prefix, X.cpu().numpy(), U.cpu().numpy(), np.arange(X.shape[0]), Ts)
     return X, U, st
+
+
+def write_csv(out_prefix, X, U, ids, Ts):
+    """``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` in the reference schema (see frames)."""
+    clean, noisy = frames(X, U, ids, Ts)
+    clean.to_csv(f"{out_prefix}_clean.csv", index=False)
+    noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
 
 
 def load_vehicle_dataset(noisy_csv_path, clean_csv_path, T_steps=600, train_split=0.7, val_split=0.15, seed=42,
