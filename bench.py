@@ -82,6 +82,7 @@ def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):
 # KalmanNet (BASELINE.json configs[4]): 1024 sequences x 200 steps, Ts = 0.01, float32
 KNET_FLOP_PER_SEQ_STEP = 2 * 3_178_373     # MACs of one gain-network step x 2
 FP32_MFMA_PEAK_TFS = 157.3                 # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+# fixed clamp limits for the tools' synthetic-input KalmanNet runs (the bench derives its own from data)
 KNET_LIMITS = {"x_min": -5.0, "x_max": 40.0, "y_min": -6.0, "y_max": 6.0, "phi_min": -3.2, "phi_max": 3.2,
                "vx_min": 0.0, "vx_max": 3.0, "vy_min": -1.0, "vy_max": 1.0, "omega_min": -6.0, "omega_max": 6.0}
 
@@ -94,29 +95,38 @@ def knet_fc2_flop(B, model):
 
 def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
                  traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r01.json")):
-    """Sequences/s of KalmanNet inference (random-init weights of the reference architecture,
-    synthetic normalized inputs resident on the GPU), all T fused steps replayed as one HIP graph.
-    The roofline object is the dominant kernel's (knet_fc2_kernel, f32 MFMA), timed with events over
-    standalone launches on the same data."""
+    """Sequences/s of KalmanNet inference (BASELINE.json configs[4]) on 1024 noisy closed-loop
+    trajectories x 200 steps at Ts = 0.01 generated on the GPU (knet_eval.make_sequences: the dataset
+    emitter's closed loop + the reference's measurement noise), normalization and clamp limits from a
+    separate train draw, seeded-init weights of the reference architecture, all T fused steps replayed
+    as one HIP graph.  The same run's posteriors give KalmanNet's MSE (test_vehicle.py:143-158), set
+    beside the EKF baseline's on the same measurements.  The roofline object is the dominant kernel's
+    (knet_fc2_kernel, f32 MFMA), timed with events over standalone launches on the same data."""
     from trajectory_generation_amd import knet as K
+    from trajectory_generation_amd import knet_eval as KE
+    Ts = 0.01
+    train = KE.make_sequences(B, T, Ts=Ts, seed=1, id_offset=KE.TRAIN_ID_OFFSET, device=dev)
+    test = KE.make_sequences(B, T, Ts=Ts, seed=0, device=dev)
+    xm, xs, ym, ys, lim = KE.normalization(train)
     torch.manual_seed(0)
-    sysm = K.VehicleModel(0.01, T, T, torch.zeros(6, 1))
-    sysm.Params.update(KNET_LIMITS)
+    sysm = K.VehicleModel(Ts, T, T, torch.zeros(6, 1))
+    sysm.Params.update(lim)
     model = K.KalmanNetNN(dev)
     model.NNBuild(sysm, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128)
-    model.set_normalization(torch.zeros(1, 6, 1), torch.ones(1, 6, 1), torch.zeros(1, 5, 1), torch.ones(1, 5, 1))
+    model.set_normalization(xm, xs, ym, ys)
     model.eval()
-    g = torch.Generator(device="cpu").manual_seed(1)
-    y = torch.randn((B, 5, T), generator=g).to(dev)
-    u = (0.2 * torch.randn((B, 2, T), generator=g)).to(dev)
-    m1x0 = (0.5 * torch.randn((B, 6, 1), generator=g)).to(dev)
+    y = ((test["y"] - ym) / ys).contiguous()
+    u = test["u"].contiguous()
+    m1x0 = KE.hybrid_init(y)
+    x_tgt = (test["x"] - xm) / xs
     run = K.KNetSequenceRunner(model, B)
+    post = {}
 
     def timed(**kw):
         run.run(y, u, m1x0, **kw)        # capture + warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run.run(y, u, m1x0, **kw)
+        post[kw.get("fused")] = run.run(y, u, m1x0, **kw)
         torch.cuda.synchronize()
         return time.perf_counter() - t0
 
@@ -149,11 +159,18 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
             traffic = None
     dt_step_graph = timed(fused=False)   # module-level step (per-layer launches), one-step graph
     achieved = KNET_FLOP_PER_SEQ_STEP * B * T / dt / 1e12
+    knet_mse, knet_db = KE.mse_and_db(post[True], x_tgt, xm, xs)
+    mod_mse, _ = KE.mse_and_db(post[False], x_tgt, xm, xs)
+    _, ekf_mse, ekf_db = KE.ekf_vs_truth(sysm.Params, Ts, test, xm, xs, ym, ys)
     out = {"metric": f"KalmanNet seq/s (B={B}, T={T})", "value": B / dt, "unit": "sequences/s",
            "ms_per_step": 1e3 * dt / T, "dtype": "f32", "path": "fused (KNetSequenceRunner.run(fused=True))",
            "module_step_graph_value": B / dt_step_graph,
-           "config": {"workload": "KalmanNetNN inference (in_mult 5, out_mult 40, hidden 128), random-init weights, "
-                                  "synthetic normalized inputs", "batch": B, "T": T, "Ts": 0.01},
+           "config": {"workload": "KalmanNetNN inference (in_mult 5, out_mult 40, hidden 128), seeded-init weights, "
+                                  "noisy closed-loop MPC trajectories (knet_eval.make_sequences)", "batch": B, "T": T,
+                      "Ts": Ts},
+           "mse": knet_mse, "mse_db": knet_db, "mse_module_path": mod_mse, "ekf_mse": ekf_mse, "ekf_mse_db": ekf_db,
+           "mse_note": "test_vehicle.py:15-40/149-158 loss on the same 1024 x 200 measurements; KalmanNet weights "
+                       "are the seeded init (no trained weights ship), the EKF is the build's baseline (f2)",
            "roofline": {"bound": "mfma", "achieved": fc2_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": fc2_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
                         "kernel": "knet_fc2_kernel<5> (FC2: Linear 256->10240, ReLU, Linear 10240->30)",
@@ -165,17 +182,18 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
         import oracle.knet_oracle as KO  # test infrastructure: CPU-baseline leg only
         w = {k: v.detach().cpu() for k, v in model.state_dict().items()}
         p = dict(KO.PARAMS)
-        p.update(KNET_LIMITS)
+        p.update(lim)
         threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
         torch.set_num_threads(threads)
-        z6, o6, z5, o5 = np.zeros((1, 6, 1)), np.ones((1, 6, 1)), np.zeros((1, 5, 1)), np.ones((1, 5, 1))
         t0 = time.perf_counter()
-        KO.run_sequences(w, p, 0.01, y[:, :, :cpu_T].cpu().numpy(), u[:, :, :cpu_T].cpu().numpy(),
-                         m1x0.cpu().numpy(), z6, o6, z5, o5)
+        KO.run_sequences(w, p, Ts, y[:, :, :cpu_T].cpu().numpy(), u[:, :, :cpu_T].cpu().numpy(),
+                         m1x0.cpu().numpy(), *(a.cpu().numpy() for a in (xm, xs, ym, ys)))
         dtc = (time.perf_counter() - t0) * (T / cpu_T)
         out["cpu_baseline"] = {"value": B / dtc, "unit": "sequences/s", "cores": threads, "kind": "port",
                                "sample": f"{B} sequences x {cpu_T} steps (scaled to T={T}), oracle/knet_oracle.py "
-                                         f"(torch CPU float32, {threads} threads)"}
+                                         f"(torch CPU float32, {threads} threads); on the 8-thread build host it runs "
+                                         f"at the speed of the reference's own KalmanNetNN (199 vs 201 seq/s, "
+                                         f"tools/knet_cpu_vs_reference.py)"}
     return out
 
 

@@ -157,3 +157,51 @@ def test_ekf_vs_oracle_and_filters(gpu):
     mse_meas = np.mean((Y - X[:, [0, 1, 3, 4, 5], :]) ** 2)
     mse_ekf = np.mean((est[:, [0, 1, 3, 4, 5], 5:] - X[:, [0, 1, 3, 4, 5], 5:]) ** 2)
     assert mse_ekf < mse_meas
+
+
+def test_config5_evaluation_pipeline(gpu):
+    """knet_eval (configs[4] MSE report): the sequences are the emitter's closed loop plus the reference's
+    noise draw (generation_type1.py:312-320), the loss is test_vehicle.py's (checked against a numpy
+    restatement), and on those measurements the EKF filters (its loss is below the raw measurements')
+    while the seeded-init KalmanNet gives a finite loss."""
+    from trajectory_generation_amd import dataset as D
+    from trajectory_generation_amd import knet as K
+    from trajectory_generation_amd import knet_eval as KE
+    B, T, Ts = 16, 40, 0.01
+    test = KE.make_sequences(B, T, Ts=Ts, seed=0)
+    train = KE.make_sequences(B, T, Ts=Ts, seed=1, id_offset=KE.TRAIN_ID_OFFSET)
+    assert test["y"].shape == (B, 5, T) and test["u"].shape == (B, 2, T) and test["x"].shape == (B, 6, T)
+    assert (test["status"] <= 1).all()
+    noise = np.stack([D.measurement_noise(i, T + 1)[:T] for i in test["ids"]])        # [B,T,6]
+    dy = (test["y"] - test["x"][:, [0, 1, 3, 4, 5], :]).cpu().numpy().astype(np.float64)
+    np.testing.assert_allclose(dy, noise[:, :, [0, 1, 3, 4, 5]].transpose(0, 2, 1), atol=1e-5)
+    xm, xs, ym, ys, lim = KE.normalization(train)
+    assert lim["vx_min"] <= float(train["x"][:, 3].min()) and lim["vx_max"] >= float(train["x"][:, 3].max())
+    # loss = numpy restatement of test_vehicle.py:15-40
+    a = torch.randn(B, 6, T, device=xm.device)
+    b = torch.randn(B, 6, T, device=xm.device)
+    an, bn = a.cpu().numpy().astype(np.float64), b.cpu().numpy().astype(np.float64)
+    xmn, xsn = xm.cpu().numpy().astype(np.float64), xs.cpu().numpy().astype(np.float64)
+    dphi = (an * xsn + xmn)[:, 2] - (bn * xsn + xmn)[:, 2]
+    ref = 5 / 6 * np.mean((an - bn)[:, [0, 1, 3, 4, 5]] ** 2) + 1 / 6 * np.mean(np.arctan2(np.sin(dphi), np.cos(dphi)) ** 2)
+    loss, db = KE.mse_and_db(a, b, xm, xs)
+    assert abs(loss - ref) <= 1e-5 * ref and abs(db - 10 * np.log10(ref)) <= 1e-4
+    params = dict(K.Params)
+    params.update(lim)
+    _, ekf_loss, _ = KE.ekf_vs_truth(params, Ts, test, xm, xs, ym, ys)
+    y_norm = (test["y"] - ym) / ys
+    # raw measurements as the estimate of the measured channels (in the state normalization)
+    yx = (test["y"] - xm[:, [0, 1, 3, 4, 5]]) / xs[:, [0, 1, 3, 4, 5]]
+    meas_loss = float(((yx - ((test["x"] - xm) / xs)[:, [0, 1, 3, 4, 5], :]) ** 2).mean())
+    assert ekf_loss < meas_loss
+    torch.manual_seed(0)
+    sysm = K.VehicleModel(Ts, T, T, torch.zeros(6, 1))
+    sysm.Params.update(lim)
+    model = K.KalmanNetNN(xm.device)
+    model.NNBuild(sysm)
+    model.set_normalization(xm, xs, ym, ys)
+    model.eval()
+    post = K.KNetSequenceRunner(model, B).run(y_norm.contiguous(), test["u"].contiguous(), KE.hybrid_init(y_norm),
+                                              fused=True)
+    kl, _ = KE.mse_and_db(post, (test["x"] - xm) / xs, xm, xs)
+    assert np.isfinite(kl)

@@ -22,6 +22,9 @@
 #ifndef TGMPC_PRIO_ITERS
 #define TGMPC_PRIO_ITERS 100   // fused run: ADMM iterations after which a solve's wave takes issue priority
 #endif
+#ifndef TGMPC_PRIO_LAG
+#define TGMPC_PRIO_LAG 0       // fused run: items of instances >= this many steps behind the draw front run at priority 3
+#endif
 #ifndef TGMPC_PRIO_RANK
 #define TGMPC_PRIO_RANK 0      // fused run: heaviest ranks (per mille of B) whose items run at priority 2
 #endif
@@ -124,6 +127,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 }
             }
         }
+#if TGMPC_PRIO_LAG > 0
+        // the queue's draw front when this item can start: an instance that lags the front by whole
+        // steps is the launch's critical chain (the run ends with it) -- its wave issues first
+        if (threadIdx.x == 0) s_item = __hip_atomic_load(&a.queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_item / a.B - step >= TGMPC_PRIO_LAG) __builtin_amdgcn_s_setprio(3);
+#endif
         __syncthreads();
         if (a.dbg_items && threadIdx.x == 0) {   // diagnostics: item timeline (traj_debug_set_item_stamps)
             a.dbg_items[4 * (size_t)q + 1] = __builtin_amdgcn_s_memrealtime();
