@@ -189,6 +189,22 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
  * same workspace (a run clears the flag when it starts). */
 int traj_closed_loop_check(const void* workspace, size_t workspace_bytes, int B, int N, void* stream);
 
+/* ---- dataset files (host memory) ----
+ * traj_dataset_write_csv: the reference's CSV schema (generation_type1.py:139-158), written with nthreads
+ * threads.  X [B,T+1,6] states, U [B,T,2] controls, noise [B,T+1,6] measurement noise (noisy file only),
+ * ids [B] trajectory ids; row r of trajectory b has t = r * Ts, the last row's d / delta empty (NaN).
+ * Either path may be NULL.  Floats are written as pandas' to_csv writes float64 (shortest round-trip
+ * repr), so the files are byte-identical to the pandas writer's.  Replaces the per-trajectory
+ * DataFrame concat + to_csv of generation_type1.py:295-339. */
+int traj_dataset_write_csv(const char* clean_path, const char* noisy_path, int B, int T, double Ts,
+                           const double* X, const double* U, const double* noise, const long long* ids,
+                           int nthreads);
+/* Data rows (header excluded) and columns of a CSV file; negative TRAJ_E_* on error. */
+long long traj_dataset_csv_rows(const char* path, int* ncols);
+/* All fields of the data rows as float64, row-major [rows, ncols] into out (e.g. pinned host memory);
+ * empty fields are NaN.  The parse of data_loader.py:5-53's pd.read_csv, in nthreads threads. */
+int traj_dataset_read_csv(const char* path, long long rows, int ncols, double* out, int nthreads);
+
 /* ---- diagnostics ----
  * Subsequent MPC launches write, per instance b, 32 int64 slots at buf[32 b ..] (device memory):
  * [0..7] s_memtime at phase boundaries (start, inputs, rollout, linearization, condensing,

@@ -114,3 +114,47 @@ def test_pack_unpack_history():
     st = torch.randint(0, 7, (T, B), dtype=torch.int32)
     X2, U2, st2 = D.unpack_history(D.pack_history(X, U, st))
     assert torch.equal(X2, X) and torch.equal(U2, U) and torch.equal(st2, st)
+
+
+def _tricky_history(B=5, T=7, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(B, T + 1, 6)) * np.array([1, 1e-5, 1e17, 3, 1e-3, 1.0])
+    X[0, 0, 0], X[0, 1, 0], X[1, 2, 1], X[1, 3, 1] = 0.0, -0.0, 1e16, 9999999999999998.0
+    X[2, 4, 3], X[2, 5, 3], X[3, 3, 3], X[4, 1, 5] = 0.0001, 0.00001, 123456.0, -2.5e-300
+    U = rng.normal(size=(B, T, 2))
+    U[0, 0, 0] = 1.0
+    return X, U
+
+
+def test_native_csv_writer_is_byte_identical_to_pandas(tmp_path):
+    """traj_dataset_write_csv (multi-threaded, host) writes the same bytes as frames() + DataFrame.to_csv:
+    Python-repr floats (fixed / exponent forms, signed zero, 1e16 boundary), empty NaN fields, global ids."""
+    X, U = _tricky_history()
+    ids = np.arange(40, 45)
+    D.write_csv(str(tmp_path / "nat"), X, U, ids, 0.05, native=True, nthreads=3)
+    D.write_csv(str(tmp_path / "pd"), X, U, ids, 0.05, native=False)
+    for s in ("clean", "noisy"):
+        assert (tmp_path / f"nat_{s}.csv").read_bytes() == (tmp_path / f"pd_{s}.csv").read_bytes(), s
+
+
+def test_native_loader_matches_pandas_loader(tmp_path):
+    """load_vehicle_dataset(native=True): the library's parser + numpy grouping gives the pandas path's
+    tensors bit for bit (data_loader.py:5-109 semantics), here on shuffled row order and extra rows."""
+    import pandas as pd
+    rng = np.random.default_rng(1)
+    B, T = 12, 30
+    X = np.cumsum(rng.normal(size=(B, T + 1, 6)) * 0.01, axis=1)
+    U = rng.normal(size=(B, T, 2)) * 0.1
+    p = str(tmp_path / "ds")
+    D.write_csv(p, X, U, np.arange(B), 0.05)
+    for s in ("clean", "noisy"):                       # rows out of order: the loader groups by id
+        df = pd.read_csv(f"{p}_{s}.csv")
+        df.sample(frac=1.0, random_state=3).sort_values("trajectory_id", kind="stable").to_csv(f"{p}_{s}.csv", index=False)
+    a = D.load_vehicle_dataset(f"{p}_noisy.csv", f"{p}_clean.csv", T_steps=25, native=True)
+    b = D.load_vehicle_dataset(f"{p}_noisy.csv", f"{p}_clean.csv", T_steps=25)
+    for pa, pb in zip(a, b):
+        for ta, tb in zip(pa, pb):
+            assert ta.dtype == torch.float32 and torch.equal(ta.isnan(), tb.isnan())   # shuffled: last rows inside
+            assert torch.equal(ta.nan_to_num(), tb.nan_to_num())
+    assert D.load_vehicle_dataset(f"{p}_noisy.csv", f"{p}_clean.csv", T_steps=40, native=True) is None
+    assert D.load_vehicle_dataset(str(tmp_path / "missing.csv"), f"{p}_clean.csv", native=True) is None

@@ -540,3 +540,21 @@ def test_dataset_generate_single_rank(gpu, oracle_lib, tmp_path):
     assert len(clean) == B * (T + 1) and list(noisy.columns)[-1] == "trajectory_id"
     np.testing.assert_allclose(clean["phi"].to_numpy().reshape(B, T + 1), X[:, :, 2].cpu().numpy(), rtol=0, atol=0)
     np.testing.assert_allclose(clean["d"].to_numpy().reshape(B, T + 1)[:, :T], U[:, :, 0].cpu().numpy(), rtol=0, atol=0)
+
+
+def test_native_loader_to_device(gpu, tmp_path):
+    """f3 device path: load_vehicle_dataset(native=True, device='cuda') parses both CSVs with the library's
+    parallel parser and copies the [n, C, T] float32 blocks from pinned memory to the GPU; the tensors
+    equal the pandas loader's (data_loader.py:5-109) bit for bit."""
+    from trajectory_generation_amd import dataset as D
+    rng = np.random.default_rng(5)
+    B, T = 40, 60
+    X = np.cumsum(rng.normal(size=(B, T + 1, 6)) * 0.01, axis=1)
+    U = rng.normal(size=(B, T, 2)) * 0.1
+    p = str(tmp_path / "ds")
+    D.write_csv(p, X, U, np.arange(B), 0.01)
+    a = D.load_vehicle_dataset(f"{p}_noisy.csv", f"{p}_clean.csv", T_steps=50, native=True, device="cuda")
+    b = D.load_vehicle_dataset(f"{p}_noisy.csv", f"{p}_clean.csv", T_steps=50)
+    for pa, pb in zip(a, b):
+        for ta, tb in zip(pa, pb):
+            assert ta.is_cuda and torch.equal(ta.cpu(), tb)

@@ -109,6 +109,10 @@ _SIGS = {
     "traj_debug_spin_limit": (C.c_int, [C.c_int]),
     "traj_debug_set_item_stamps": (C.c_int, [_V]),
     "traj_closed_loop_check": (C.c_int, [_V, C.c_size_t, C.c_int, C.c_int, _V]),
+    "traj_dataset_write_csv": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_double, _V, _V, _V, _V,
+                                         C.c_int]),
+    "traj_dataset_csv_rows": (C.c_longlong, [C.c_char_p, _V]),
+    "traj_dataset_read_csv": (C.c_int, [C.c_char_p, C.c_longlong, C.c_int, _V, C.c_int]),
     "traj_debug_kernel_times": (C.c_int, [_V, _V]),
     "traj_knet_prior_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float, C.c_int,
                                       _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),

@@ -130,15 +130,53 @@ def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=N
     return X, U, st
 
 
-def write_csv(out_prefix, X, U, ids, Ts):
-    """``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` in the reference schema (see frames)."""
-    clean, noisy = frames(X, U, ids, Ts)
-    clean.to_csv(f"{out_prefix}_clean.csv", index=False)
-    noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
+def write_csv(out_prefix, X, U, ids, Ts, native=True, nthreads=None):
+    """``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` in the reference schema (see frames).
+    native: the library's multi-threaded writer (traj_dataset_write_csv), byte-identical to the pandas
+    writer (native=False, frames + DataFrame.to_csv)."""
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    U = np.ascontiguousarray(U, dtype=np.float64)
+    if not native:
+        clean, noisy = frames(X, U, ids, Ts)
+        clean.to_csv(f"{out_prefix}_clean.csv", index=False)
+        noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
+        return
+    import ctypes as C
+    import os
+    from . import _lib
+    B, n_rows = X.shape[0], X.shape[1]
+    noise = np.ascontiguousarray(np.stack([measurement_noise(i, n_rows) for i in ids]) if B else
+                                 np.zeros((0, n_rows, 6)))
+    ids64 = np.ascontiguousarray(ids, dtype=np.int64)
+    nt = int(nthreads or min(16, os.cpu_count() or 1))
+    p = lambda a: C.c_void_p(a.ctypes.data)   # noqa: E731
+    _lib.check(_lib.lib().traj_dataset_write_csv(f"{out_prefix}_clean.csv".encode(), f"{out_prefix}_noisy.csv".encode(),
+                                                 B, n_rows - 1, float(Ts), p(X), p(U), p(noise), p(ids64), nt),
+               "traj_dataset_write_csv")
+
+
+def read_csv_native(path, nthreads=None, pin=False):
+    """All columns of a dataset CSV as {name: float64 array} through the library's parallel parser
+    (traj_dataset_read_csv) into one [rows, C] buffer -- pinned host memory with pin=True."""
+    import ctypes as C
+    import os
+    import torch
+    from . import _lib
+    with open(path) as f:
+        names = f.readline().strip().split(",")
+    nc = C.c_int(0)
+    rows = int(_lib.lib().traj_dataset_csv_rows(str(path).encode(), C.byref(nc)))
+    if rows < 0 or nc.value != len(names):
+        raise ValueError(f"{path}: not a dataset CSV ({rows}, {nc.value} columns)")
+    buf = torch.empty((rows, len(names)), dtype=torch.float64, pin_memory=pin)
+    nt = int(nthreads or min(16, os.cpu_count() or 1))
+    _lib.check(_lib.lib().traj_dataset_read_csv(str(path).encode(), rows, len(names), C.c_void_p(buf.data_ptr()), nt),
+               "traj_dataset_read_csv")
+    return names, buf
 
 
 def load_vehicle_dataset(noisy_csv_path, clean_csv_path, T_steps=600, train_split=0.7, val_split=0.15, seed=42,
-                         device=None):
+                         device=None, native=False):
     """KalmanNet/data_loader.py:5-109 (load_vehicle_dataset), vectorized: the first T_steps rows of every
     trajectory (ids 0..n-1), y = noisy [X, Y, vx, vy, omega], u = [d, delta], x = clean
     [X, Y, phi, vx, vy, omega] as float32 [n, C, T]; trajectories shuffled by default_rng(seed) and split
@@ -146,6 +184,8 @@ def load_vehicle_dataset(noisy_csv_path, clean_csv_path, T_steps=600, train_spli
     when a file or a trajectory is missing, as the reference does."""
     import pandas as pd
     import torch
+    if native:
+        return _load_native(noisy_csv_path, clean_csv_path, T_steps, train_split, val_split, seed, device)
     try:
         dn = pd.read_csv(noisy_csv_path)
         dc = pd.read_csv(clean_csv_path)
@@ -178,3 +218,48 @@ def load_vehicle_dataset(noisy_csv_path, clean_csv_path, T_steps=600, train_spli
     for part in zip(cut(y), cut(u), cut(x)):
         out.append(tuple(torch.tensor(np.ascontiguousarray(p), dtype=torch.float32, device=device) for p in part))
     return tuple(out)
+
+
+def _load_native(noisy_csv_path, clean_csv_path, T_steps, train_split, val_split, seed, device):
+    """load_vehicle_dataset with the library's parser: both files parsed in parallel into pinned host
+    buffers, grouped per trajectory with numpy (first T_steps rows of ids 0..n-1, data_loader.py:14-53),
+    the three [n, C, T] float32 blocks copied to `device` from pinned memory."""
+    import os
+    import torch
+    if not (os.path.exists(noisy_csv_path) and os.path.exists(clean_csv_path)):
+        return None
+    pin = device is not None and torch.device(device).type == "cuda"
+    blocks = []
+    n = None
+    for path, cols in ((noisy_csv_path, (["X", "Y", "vx", "vy", "omega"], ["d", "delta"])),
+                       (clean_csv_path, (["X", "Y", "phi", "vx", "vy", "omega"],))):
+        names, buf = read_csv_native(path, pin=False)
+        a = buf.numpy()
+        tid = a[:, names.index("trajectory_id")].astype(np.int64)
+        if n is None:
+            n = int(np.unique(tid).size)
+        keep = np.nonzero(tid < n)[0]
+        order = keep[np.argsort(tid[keep], kind="stable")]
+        counts = np.bincount(tid[keep], minlength=n)
+        if counts.size != n or (counts < T_steps).any():
+            return None
+        first = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        rows = order[(first[:, None] + np.arange(T_steps)[None, :]).reshape(-1)]
+        for cl in cols:
+            idx = [names.index(c) for c in cl]
+            blk = a[rows][:, idx].astype(np.float32).reshape(n, T_steps, len(cl)).transpose(0, 2, 1)
+            blocks.append(np.ascontiguousarray(blk))
+    y, u, x = blocks
+    idx = np.arange(n)
+    np.random.default_rng(seed).shuffle(idx)
+    y, u, x = y[idx], u[idx], x[idx]
+    n_tr, n_va = int(n * train_split), int(n * val_split)
+    cut = lambda a: (a[:n_tr], a[n_tr:n_tr + n_va], a[n_tr + n_va:])   # noqa: E731
+
+    def dev(a):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if pin:
+            return t.pin_memory().to(device, non_blocking=True)
+        return t.to(device) if device is not None else t
+
+    return tuple(tuple(dev(p) for p in part) for part in zip(cut(y), cut(u), cut(x)))
