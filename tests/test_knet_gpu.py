@@ -12,15 +12,15 @@ pytestmark = pytest.mark.gpu
 G = np.load("tests/golden/knet.npz")
 
 
-def build(dev, seed=0):
+def build(dev, seed=0, in_mult=5):
     from trajectory_generation_amd import knet as K
     sysm = K.VehicleModel(float(G["Ts"]), 20, 20, torch.zeros(6, 1))
     sysm.Params.update(LIMITS)
     model = K.KalmanNetNN(dev)
-    model.NNBuild(sysm, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128)
+    model.NNBuild(sysm, in_mult_KNet=in_mult, out_mult_KNet=40, hidden_dim_gru=128)
     f32 = lambda a: torch.tensor(a, dtype=torch.float32)   # noqa: E731
     model.set_normalization(f32(G["x_mean"]), f32(G["x_std"]), f32(G["y_mean"]), f32(G["y_std"]))
-    sd = {k: torch.tensor(v) for k, v in knet_weights(seed=seed).items()}
+    sd = {k: torch.tensor(v) for k, v in knet_weights(seed=seed, in_mult=in_mult).items()}
     model.load_state_dict(sd, strict=True)
     model.eval()
     return K, sysm, model
@@ -96,13 +96,16 @@ def test_graph_runner_matches_eager_and_oracle(gpu):
     assert np.abs(eager - ref).max() <= 1e-3 * (1 + np.abs(ref).max())
 
 
-@pytest.mark.parametrize("B,T,groups", [(64, 30, 1), (7, 5, 1), (1, 3, 1), (37, 6, 3)])
-def test_fused_runner_vs_oracle(gpu, B, T, groups):
+@pytest.mark.parametrize("B,T,groups,in_mult", [(64, 30, 1, 5), (7, 5, 1, 5), (1, 3, 1, 5), (37, 6, 3, 5),
+                                                 (64, 30, 1, 10), (37, 6, 3, 10)])
+def test_fused_runner_vs_oracle(gpu, B, T, groups, in_mult):
     """Fused step (traj_knet_front_f32 / FC2 GEMMs / traj_knet_back_f32, whole-T graph) vs the CPU oracle,
-    ragged batches (B not a multiple of the 4 sequences a workgroup owns) included."""
+    ragged batches (B not a multiple of the 4 sequences a workgroup owns) included, for the reference's two
+    architectures (in_mult 5: test_vehicle.py / training_prediction.py; 10: training.py / test_prediction.py,
+    FC5 60 wide)."""
     from oracle import knet_oracle as KO
     from trajectory_generation_amd.knet import KNetSequenceRunner
-    _, sysm, model = build(gpu, seed=1)
+    _, sysm, model = build(gpu, seed=1, in_mult=in_mult)
     rng = np.random.default_rng(11 + B)
     y = torch.tensor(rng.normal(size=(B, 5, T)), dtype=torch.float32, device=gpu)
     u = torch.tensor(np.stack([rng.uniform(0, 0.5, (B, T)), rng.uniform(-0.3, 0.3, (B, T))], 1), dtype=torch.float32,
@@ -120,9 +123,9 @@ def test_fused_runner_vs_oracle(gpu, B, T, groups):
     np.testing.assert_array_equal(fs, f0)
     p = dict(KO.PARAMS)
     p.update(LIMITS)
-    ref = KO.run_sequences(knet_weights(1), p, float(G["Ts"]), y.cpu().numpy(), u.cpu().numpy(), m1x0.cpu().numpy(),
-                           G["x_mean"], G["x_std"], G["y_mean"], G["y_std"]).numpy()
-    t = 1e-3 * (1 + np.abs(ref).max())
+    ref = KO.run_sequences(knet_weights(1, in_mult=in_mult), p, float(G["Ts"]), y.cpu().numpy(), u.cpu().numpy(),
+                           m1x0.cpu().numpy(), G["x_mean"], G["x_std"], G["y_mean"], G["y_std"]).numpy()
+    t = 2e-4 * (1 + np.abs(ref).max())
     assert np.abs(f0 - ref).max() <= t
     assert np.abs(f0 - eager).max() <= t
 

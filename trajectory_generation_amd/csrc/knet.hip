@@ -762,7 +762,8 @@ __global__ __launch_bounds__(KT) void knet_back_front_kernel(KNet net, int B, co
     // FC3 has at most 64 units, so units 64..127 are idle once its partials are published: there they
     // run step t + 1's FC5 (on the prior) and FC7 (on the innovation), one output per thread, instead of
     // two more layer stages after FC4.
-    const bool side = net.dFC3 <= 64 && net.m <= 16 && net.n <= 16 && (net.dFC5 + net.dFC7) * KS <= 4 * KT / 2;
+    // (fc57's loop strides over any number of FC5 / FC7 outputs: in_mult 10's 60 + 5 units included)
+    const bool side = net.dFC3 <= 64 && net.m <= 16 && net.n <= 16;
     auto fc57 = [&]() {
         if (!side || (t & (KH - 1)) < 64) return;
         const int i = (t >> 7) * 64 + (t & 63);
@@ -984,8 +985,9 @@ int traj_knet_update_f32(int B, const float* x_prior, const float* KG, const flo
 }
 
 static bool knet_ok(const traj_knet_net* w) {
-    return w && w->m == 6 && w->n == 5 && w->hidden == KH && w->d_fc5 > 0 && w->d_fc5 <= 32 && w->d_fc1 > 0 &&
-           w->d_fc7 > 0 && w->d_fc1 + w->d_fc7 <= 32 && w->d_fc3 > 0 && w->d_fc3 <= 64 && w->fc5_w && w->fc5_b &&
+    // FC5 / [FC1 | FC7] outputs live in 64-wide zero-padded LDS rows: in_mult 5 and 10 (d_fc5 30 / 60)
+    return w && w->m == 6 && w->n == 5 && w->hidden == KH && w->d_fc5 > 0 && w->d_fc5 <= 64 && w->d_fc1 > 0 &&
+           w->d_fc7 > 0 && w->d_fc1 + w->d_fc7 <= 64 && w->d_fc3 > 0 && w->d_fc3 <= 64 && w->fc5_w && w->fc5_b &&
            w->gru_q_wih && w->gru_q_bih && w->gru_q_whh && w->gru_q_bhh && w->gru_sigma_wih && w->gru_sigma_bih &&
            w->gru_sigma_whh && w->gru_sigma_bhh && w->fc1_w && w->fc1_b && w->fc7_w && w->fc7_b && w->gru_s_wih &&
            w->gru_s_bih && w->gru_s_whh && w->gru_s_bhh && w->fc3_w && w->fc3_b && w->fc4_w && w->fc4_b && w->innov_logit &&
