@@ -84,13 +84,20 @@ __device__ __forceinline__ Tire tire_angles(const VP& p, double vx, double vy, d
     r.atr = atan2(omega * p.lr - vy, r.vx_eff);
     return r;
 }
+// The Pacejka sine as the sine of sincos: the lane-parallel chains of block_linearize evaluate
+// sincos for every lane (the phi lanes need the cosine), so the per-step kernels take the same value.
+__device__ __forceinline__ double tire_sin(double z) {
+    double s, c;
+    sincos(z, &s, &c);
+    return s;
+}
 __device__ __forceinline__ double front_force(const VP& p, double atf, double delta) {
     const double alpha_f = clampd(-atf + delta, -p.maxAlpha, p.maxAlpha);
-    return p.Df * sin(p.Cf * atan(p.Bf * alpha_f));
+    return p.Df * tire_sin(p.Cf * atan(p.Bf * alpha_f));
 }
 __device__ __forceinline__ double rear_force(const VP& p, double atr) {
     const double alpha_r = clampd(atr, -p.maxAlpha, p.maxAlpha);
-    return p.Dr * sin(p.Cr * atan(p.Br * alpha_r));
+    return p.Dr * tire_sin(p.Cr * atan(p.Br * alpha_r));
 }
 __device__ __forceinline__ double long_force(const VP& p, double vx, double d) {
     return (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
@@ -238,35 +245,60 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 }
 
 // In-workgroup linearization for the fused closed loop (traj_closed_loop_run): rollout_kernel's
-// and jac_kernel's arithmetic (the same device functions) for ONE instance and NT threads, with
-// A_k, B_k, g_k written to LDS in the solve kernel's staging layout.  xs / us: the state and input
-// (LDS); xf: scratch [N][12] (LDS).  Ends with a workgroup barrier.
+// and jac_kernel's arithmetic for ONE instance and NT threads, with A_k, B_k, g_k written to LDS in the
+// solve kernel's staging layout.  xs / us: the state and input (LDS); xf: scratch [N][12] (LDS);
+// tj: scratch [N][TJ] (LDS) for the Jacobian's tire / sincos evaluations.  Ends with a barrier.
+//
+// The rollout is a serial chain: per stage, atan2 -> atan -> sincos on three lanes.  The Jacobian
+// columns of stage k need the same chain at perturbed copies of x_k, known as soon as x_k is: lanes
+// 3 .. 21 run those evaluations IN THE SAME instruction stream as the rollout lanes (the stage's
+// latency does not change; round 1 ran them as a separate 29 k-cycle pass).  Lane roles, stage k:
+//   0 / 1 / 2   rollout: front tire, rear tire, sincos(phi) at x_k (raw, rollout_kernel's form)
+//   3 / 4       base front / rear tire at x_k + 0.0 (cheap_columns' t0)
+//   5 .. 16     4 lanes per state column (vx, vy, omega): (+eps front, +eps rear, -eps front, -eps rear)
+//   17 / 18     front tire at delta +- eps (the delta column)
+//   19 / 20     sincos(phi +- eps) (the phi column);   21   sincos(phi + 0.0)
+// Their sines go to tj[k][lane], the cosines of lanes 19 .. 21 to tj[k][0 .. 2].  An assembly pass (one
+// stage per lane) then forms f at each perturbed point with f_parts and the difference quotients:
+// the values state_column / cheap_columns compute (jac_kernel), bit for bit.
+constexpr int TJ = 24;
 template <int NT>
 __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N, double Ts, const double* xs,
-                                                const double* us, double* xf, double* A, double* Bm, double* g,
-                                                long long* dbg = nullptr) {
+                                                const double* us, double* xf, double* tj, double* A, double* Bm,
+                                                double* g, long long* dbg = nullptr) {
     auto mark = [&](int i) { if (dbg && t == 0) dbg[i] = __builtin_amdgcn_s_memtime(); };
+    const double eps = 1e-5;
     if (t < 64) {
-        // rollout (rollout_kernel's arithmetic): per stage, lanes 0 / 1 / 2 run the front-tire chain,
-        // the rear-tire chain and sincos(phi) as ONE instruction stream (atan2 -> atan -> sincos),
-        // the results are broadcast with v_readlane and every lane steps the (uniform) state
         double x[6];
         for (int i = 0; i < 6; ++i) x[i] = xs[i];
         const double u0 = us[0], u1 = us[1];
         double sd, cd;
         sincos(u1, &sd, &cd);
-        const bool fr = (t == 0);
+        // this lane's role (see above): tire chain or sincos, which tire, which input it perturbs
+        const bool roll = t < 3;
+        const bool tire = (t < 2) || (t >= 3 && t <= 18);
+        const bool fr = (t == 0) || (t == 3) || (t >= 5 && t <= 16 && ((t - 5) & 1) == 0) || t == 17 || t == 18;
+        const int col = (t >= 5 && t <= 16) ? (t - 5) >> 2 : -1;             // 0 vx, 1 vy, 2 omega
+        const double sgn = (t >= 5 && t <= 16 && ((t - 5) & 2)) ? -eps : eps;
+        const double dlt = (t == 17) ? u1 + eps : ((t == 18) ? u1 - eps : u1);
+        const double pz = (t == 19) ? eps : ((t == 20) ? -eps : 0.0);
         const double Bt = fr ? p.Bf : p.Br, Ct = fr ? p.Cf : p.Cr;
         for (int k = 0; k < N; ++k) {
             const double phi = x[2], vx = x[3], vy = x[4], omega = x[5];
-            const double avx = fabs(vx);
+            // this lane's evaluation point (state_column / cheap_columns: x_i + 0.0, the column x_i +- eps)
+            const double vxl = roll ? vx : (col == 0 ? vx + sgn : vx + 0.0);
+            const double vyl = roll ? vy : (col == 1 ? vy + sgn : vy + 0.0);
+            const double oml = roll ? omega : (col == 2 ? omega + sgn : omega + 0.0);
+            const double avx = fabs(vxl);
             const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
-            const double vx_eff = np_sign(vx) * mx;
-            const double at = atan2(fr ? omega * p.lf + vy : omega * p.lr - vy, vx_eff);
-            const double alpha = clampd(fr ? -at + u1 : at, -p.maxAlpha, p.maxAlpha);
-            const double z = (t < 2) ? Ct * atan(Bt * alpha) : phi;
+            const double vx_eff = np_sign(vxl) * mx;
+            const double at = atan2(fr ? oml * p.lf + vyl : oml * p.lr - vyl, vx_eff);
+            const double alpha = clampd(fr ? -at + dlt : at, -p.maxAlpha, p.maxAlpha);
+            const double z = tire ? Ct * atan(Bt * alpha) : (t == 2 ? phi : phi + pz);
             double sz, cz;
             sincos(z, &sz, &cz);
+            if (t >= 3 && t <= 21) tj[TJ * k + t] = sz;
+            if (t >= 19 && t <= 21) tj[TJ * k + t - 19] = cz;
             const double Fy_f = p.Df * readlane_d(sz, 0), Fy_r = p.Dr * readlane_d(sz, 1);
             const double sphi = readlane_d(sz, 2), cphi = readlane_d(cz, 2);
             const double Frx = (p.Cm1 - p.Cm2 * vx) * u0 - p.Cr0 - p.Cr2 * (vx * vx);
@@ -287,37 +319,70 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
     }
     __syncthreads();
     mark(20);
-    const double d = us[0], de = us[1];
-    // vx / vy / omega columns: one (column, stage) per lane, one code path
-    for (int tau = t; tau < 3 * N; tau += NT) {
-        const int grp = tau / N, k = tau - grp * N;
-        double xb[6], J[6];
-        for (int i = 0; i < 6; ++i) xb[i] = xf[12 * k + i];
-        state_column(p, xb, d, de, grp, J);
-        const int cc = 3 + grp;
-        for (int r = 0; r < 6; ++r) A[36 * k + 6 * r + cc] = a_entry(r, cc, Ts, J[r]);
-    }
     mark(21);
-    // phi / d / delta columns, the constant X, Y columns: one stage per lane
+    const double d = us[0], de = us[1];
+    // assembly: one stage per lane -- f at every perturbed point from the stored sines (f_parts, the
+    // reference's difference quotients), A = I + Ts Jx, B = Ts Ju, g = x + Ts f - A x - B u
+    double sd, cd, sdp, cdp, sdm, cdm;
+    sincos(de, &sd, &cd);
+    sincos(de + eps, &sdp, &cdp);
+    sincos(de - eps, &sdm, &cdm);
     for (int k = t; k < N; k += NT) {
-        double xb[6], Jphi[6], Jd[6], Jde[6];
-        for (int i = 0; i < 6; ++i) xb[i] = xf[12 * k + i];
-        cheap_columns(p, xb, d, de, Jphi, Jd, Jde);
-        for (int r = 0; r < 6; ++r) {
-            A[36 * k + 6 * r + 0] = a_entry(r, 0, Ts, 0.0);
-            A[36 * k + 6 * r + 1] = a_entry(r, 1, Ts, 0.0);
-            A[36 * k + 6 * r + 2] = a_entry(r, 2, Ts, Jphi[r]);
-            Bm[12 * k + 2 * r + 0] = Ts * Jd[r];
-            Bm[12 * k + 2 * r + 1] = Ts * Jde[r];
-        }
-    }
-    __syncthreads();
-    for (int k = t; k < N; k += NT) {
-        double xb[6], fk[6], Ak[36], Bk[12], gk[6];
+        const double* T = tj + TJ * k;
+        double xb[6], fk[6];
         for (int i = 0; i < 6; ++i) { xb[i] = xf[12 * k + i]; fk[i] = xf[12 * k + 6 + i]; }
-        for (int i = 0; i < 36; ++i) Ak[i] = A[36 * k + i];
-        for (int i = 0; i < 12; ++i) Bk[i] = Bm[12 * k + i];
+        const double vx0 = xb[3] + 0.0, vy0 = xb[4] + 0.0, om0 = xb[5] + 0.0;
+        const double sphi = T[21], cphi = T[2];
+        const double Ff0 = p.Df * T[3], Fr0 = p.Dr * T[4], Fx0 = long_force(p, vx0, d);
+        double Ak[36], Bk[12], fp[6], fm[6];
+        for (int grp = 0; grp < 3; ++grp) {   // state columns (state_column)
+            const double vxp = grp == 0 ? xb[3] + eps : vx0, vxm = grp == 0 ? xb[3] - eps : vx0;
+            const double vyp = grp == 1 ? xb[4] + eps : vy0, vym = grp == 1 ? xb[4] - eps : vy0;
+            const double omp = grp == 2 ? xb[5] + eps : om0, omm = grp == 2 ? xb[5] - eps : om0;
+            const int l = 5 + 4 * grp;
+            f_parts(p, vxp, vyp, omp, sphi, cphi, sd, cd, p.Df * T[l], p.Dr * T[l + 1], long_force(p, vxp, d), fp);
+            f_parts(p, vxm, vym, omm, sphi, cphi, sd, cd, p.Df * T[l + 2], p.Dr * T[l + 3], long_force(p, vxm, d), fm);
+            for (int r = 0; r < 6; ++r) Ak[6 * r + 3 + grp] = a_entry(r, 3 + grp, Ts, (fp[r] - fm[r]) / (2.0 * eps));
+        }
+        double Jphi[6], Jd[6], Jde[6];
+        // phi: only sin / cos(phi) change
+        f_parts(p, vx0, vy0, om0, T[19], T[0], sd, cd, Ff0, Fr0, Fx0, fp);
+        f_parts(p, vx0, vy0, om0, T[20], T[1], sd, cd, Ff0, Fr0, Fx0, fm);
+        for (int r = 0; r < 6; ++r) Jphi[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        // d: only the longitudinal force changes
+        f_parts(p, vx0, vy0, om0, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx0, d + eps), fp);
+        f_parts(p, vx0, vy0, om0, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx0, d - eps), fm);
+        for (int r = 0; r < 6; ++r) Jd[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        // delta: front force and sin / cos(delta) change
+        f_parts(p, vx0, vy0, om0, sphi, cphi, sdp, cdp, p.Df * T[17], Fr0, Fx0, fp);
+        f_parts(p, vx0, vy0, om0, sphi, cphi, sdm, cdm, p.Df * T[18], Fr0, Fx0, fm);
+        for (int r = 0; r < 6; ++r) Jde[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        // a -0.0 among the components the input columns pass through: those two columns on the
+        // reference's exact vectors, as cheap_columns does
+        if ((__builtin_signbit(xb[2]) && xb[2] == 0.0) || (__builtin_signbit(xb[3]) && xb[3] == 0.0) ||
+            (__builtin_signbit(xb[4]) && xb[4] == 0.0) || (__builtin_signbit(xb[5]) && xb[5] == 0.0) ||
+            (__builtin_signbit(d) && d == 0.0) || (__builtin_signbit(de) && de == 0.0)) {
+            for (int cu = 0; cu < 2; ++cu) {
+                const double up[2] = {cu == 0 ? d + eps : d + 0.0, cu == 1 ? de + eps : de + 0.0};
+                const double um[2] = {cu == 0 ? d - eps : d + 0.0, cu == 1 ? de - eps : de + 0.0};
+                double xc[6];
+                for (int i = 0; i < 6; ++i) xc[i] = xb[i];
+                f_cont(p, xc, up, fp);
+                f_cont(p, xc, um, fm);
+                for (int r = 0; r < 6; ++r) (cu == 0 ? Jd : Jde)[r] = (fp[r] - fm[r]) / (2.0 * eps);
+            }
+        }
+        for (int r = 0; r < 6; ++r) {
+            Ak[6 * r + 0] = a_entry(r, 0, Ts, 0.0);
+            Ak[6 * r + 1] = a_entry(r, 1, Ts, 0.0);
+            Ak[6 * r + 2] = a_entry(r, 2, Ts, Jphi[r]);
+            Bk[2 * r + 0] = Ts * Jd[r];
+            Bk[2 * r + 1] = Ts * Jde[r];
+        }
+        double gk[6];
         g_stage(Ak, Bk, xb, fk, d, de, Ts, gk);
+        for (int i = 0; i < 36; ++i) A[36 * k + i] = Ak[i];
+        for (int i = 0; i < 12; ++i) Bm[12 * k + i] = Bk[i];
         for (int r = 0; r < 6; ++r) g[6 * k + r] = gk[r];
     }
     __syncthreads();

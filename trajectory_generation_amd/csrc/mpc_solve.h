@@ -22,6 +22,9 @@
 #ifndef TGMPC_PRIO_ITERS
 #define TGMPC_PRIO_ITERS 100   // fused run: ADMM iterations after which a solve's wave takes issue priority
 #endif
+#ifndef TGMPC_PRIO_SWEEP
+#define TGMPC_PRIO_SWEEP 0     // fused run: factorization sweeps at priority 2
+#endif
 #ifndef TGMPC_PRIO_LAG
 #define TGMPC_PRIO_LAG 0       // fused run: items of instances >= this many steps behind the draw front run at priority 3
 #endif
@@ -68,8 +71,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     double* const s_cold = s_big + NP;
     __shared__ double s_xh[(NM + 1) * 6];
     __shared__ double s_sc[(NM + 1) * 2];
-    __shared__ __attribute__((aligned(16))) double s_ex[6 * NN];   // exchange / broadcast buffers
-    __shared__ __attribute__((aligned(16))) double s_sw[2 * (2 * NN + 2)];   // sweep pivot columns
+    // one region, two lives: the solve's exchange / broadcast buffers and sweep pivot columns, or (fused,
+    // during block_linearize) the Jacobian's tire evaluations [NM][TJ]
+    constexpr int NEX = 6 * NN, NSW = 2 * (2 * NN + 2);
+    constexpr int NU = (NEX + NSW > TJ * NM) ? NEX + NSW : TJ * NM;
+    __shared__ __attribute__((aligned(16))) double s_u[NU];
+    double* const s_ex = s_u;            // exchange / broadcast buffers
+    double* const s_sw = s_u + NEX;      // sweep pivot columns (16-byte aligned: NEX is even)
     __shared__ double s_F[2 * 4 * 16 * ((NN + 15) / 16)];                    // condensing: F_k rows
     __shared__ double s_red[16 * WAVES];
     __shared__ int s_flag[4];
@@ -278,9 +286,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
     if (fused) {
         // s_F (the condensing's F rows) is the rollout record's scratch here; zeroed again after
-        block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_F, s_big, s_big + 36 * N, s_big + 48 * N,
+        block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_F, s_u, s_big, s_big + 36 * N, s_big + 48 * N,
                             a.dbg ? a.dbg + (size_t)b * 32 : nullptr);
         for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
+        for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;   // s_u held the tire evaluations
     } else if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
         // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
         // at once (one L2/MALL latency, no VGPRs); the three blocks are contiguous in s_big as double2
@@ -728,6 +737,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             // (K symmetric: K[pv][c] = K[c][pv]).  Padding pivots (>= n) are identity and exact.
             bool ok = true;
             tic();
+#if TGMPC_PRIO_SWEEP
+            if (FUSED) __builtin_amdgcn_s_setprio(2);   // the sweep's pivot chain is LDS-latency bound
+#endif
             if constexpr (WAVES == 1 && NN <= 42) {
                 // One-wave sweep, ONE fma per entry and pivot.  The new pivot row (K_pj / d) is not
                 // formed in place (that needs a second operation on the pivot lane only) but in a
@@ -847,6 +859,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #pragma unroll
             for (int j = 0; j < NN; ++j) Krow[j] = -Krow[j];
             toc(cyc_sweep);
+#if TGMPC_PRIO_SWEEP
+            if (FUSED) __builtin_amdgcn_s_setprio(0);
+#endif
             if (!ok) {
                 if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
                 // failed reduced-KKT factorization = unsuccessful polish (polish.c): the ADMM
