@@ -404,9 +404,17 @@ def main():
                 # solve_kernel is VALU-issue/latency bound: the issued f64 lane-FLOP rate against the f64
                 # vector peak, and the VALU issue slots used (4 cycles per wave64 instruction)
                 fl = ij["f64_flop_issued_per_step"] * value / world / 1e12
+                # F(N, K) = N (60 + 150) + 72 N (N + 1) + (N + 1)(72 N + 24 N^2) + 8 N^3 / 3
+                #                 + K (8 N^2 + 20 N) algorithmic f64 FLOP per step, K = mean ADMM iterations
+                K = float(iters.mean())
+                f_alg = (N * 210 + 72 * N * (N + 1) + (N + 1) * (72 * N + 24 * N * N) + 8 * N ** 3 / 3
+                         + K * (8 * N * N + 20 * N))
+                fa = f_alg * value / world / 1e12
                 issue = {"what": "solve_kernel issue side (PMC SQ_INSTS_VALU*, per instance-step x steps/s)",
                          "f64_tflops_issued": fl, "f64_peak_tflops": F64_VECTOR_PEAK_TF,
                          "f64_frac": fl / F64_VECTOR_PEAK_TF,
+                         "f64_flop_algorithmic_per_step": f_alg, "f64_tflops_algorithmic": fa,
+                         "f64_frac_algorithmic": fa / F64_VECTOR_PEAK_TF,
                          "valu_insts_per_step": ij["valu_insts_per_step"],
                          "valu_issue_frac": ij["valu_insts_per_step"] * 4 * value / world / (SIMDS * CLOCK_HZ),
                          "source": os.path.relpath(args.issue_json, HERE)}

@@ -558,3 +558,26 @@ def test_native_loader_to_device(gpu, tmp_path):
     for pa, pb in zip(a, b):
         for ta, tb in zip(pa, pb):
             assert ta.is_cuda and torch.equal(ta.cpu(), tb)
+
+
+def test_config3_hard_states_vs_fixture(gpu):
+    """Config 3's hard states (tests/golden/qp_N40_Ts005_hard.npz, recorded from the reference's own
+    rollout): the GPU step gives the fixture's statuses -- the u_prev fallback (mpc_6stati.py:257-262) on
+    every step whose reference rollout blows up -- and, where exact mode certifies its point on a control
+    row, the sparse-form (interior point) optimum to 1e-4."""
+    g = np.load("tests/golden/qp_N40_Ts005_hard.npz")
+    N, Ts = int(g["N"]), float(g["Ts"])
+    keep = np.isfinite(g["x0"]).all(axis=1)
+    x0, up, pr, vr = g["x0"][keep], g["u_prev"][keep], g["path_ref"][keep], g["vref"][keep]
+    o = TB.mpc_step_batch(x0, up, pr, vr, TB.config_struct(N=N, Ts=Ts))
+    o = {k: v.cpu().numpy() for k, v in o.items()}
+    assert np.array_equal(o["status"], g["condensed_status"][keep])
+    fail = g["failing"][keep] == 1
+    assert np.array_equal(o["u_cmd"][fail], up[fail])
+    ok = (~fail) & (g["ipm_status"][keep] == 0) & (g["ref_xbar_max"][keep] < 1e3)
+    ox = TB.mpc_step_batch(x0[ok], up[ok], pr[ok], vr[ok], TB.config_struct(N=N, Ts=Ts, polish_mode=1))
+    ox = {k: v.cpu().numpy() for k, v in ox.items()}
+    cert = ox["polished"] > 0
+    assert cert.sum() >= 16
+    du = np.abs(ox["U_opt"][cert] - g["U_opt"][keep][ok][cert]).max()
+    assert du <= 1e-4, du
