@@ -229,6 +229,10 @@ int traj_debug_fused_grid(int workgroups);
 /* Polls of an instance's step counter before a fused-run hand-off is declared lost (0: the default,
  * 2^22 polls with s_sleep back-off, seconds).  For the test that the loss is reported. */
 int traj_debug_spin_limit(int polls);
+/* Fused-run queue order: the heaviest per_mille / 1000 of the instances (by the previous launch's mean
+ * ADMM iterations) run `steps` steps ahead of the level front (default 1 step, 100 per mille; 0 = plain
+ * level order).  Results do not depend on it.  For experiments and tests. */
+int traj_debug_queue_lead(int steps, int per_mille);
 int traj_debug_kernel_times(double* ms, int* n_steps);
 
 #ifdef __cplusplus

@@ -384,6 +384,36 @@ def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
         assert torch.equal(per[k], fus2[k]), k
 
 
+@pytest.mark.parametrize("lead", [(0, 0), (3, 500), (1, 999)])
+def test_fused_queue_lead_bit_identical(gpu, lead):
+    """The fused run's queue order (heavy instances ahead of the level front, traj_debug_queue_lead) moves
+    only the schedule: a run continued from a first launch (so that the order has a previous launch to
+    rank by) equals the per-step launches bit for bit, whatever the lead."""
+    from trajectory_generation_amd import _lib
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B, T0 = 20, 0.05, 16, 80, 4
+    w = make_workload(B, N, Ts, kind="spline", seed=8)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    x = torch.as_tensor(w["x0"], device=gpu).clone()
+    u = torch.as_tensor(w["u0"], device=gpu).clone()
+    vr = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=gpu)
+    hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=gpu)
+    hu = torch.empty((B, T, 2), dtype=torch.float64, device=gpu)
+    hx[:, 0] = x
+    st = torch.empty((T, B), dtype=torch.int32, device=gpu)
+    it = torch.empty((T, B), dtype=torch.int32, device=gpu)
+    try:
+        _lib.check(_lib.lib().traj_debug_queue_lead(*lead), "traj_debug_queue_lead")
+        TB.closed_loop_run(x, u, paths, vr, cfg, None, 0, T0, hx, hu, st[:T0], it[:T0])
+        TB.closed_loop_run(x, u, paths, vr, cfg, None, T0, T - T0, hx, hu, st[T0:], it[T0:])
+    finally:
+        _lib.lib().traj_debug_queue_lead(1, 100)
+    assert torch.equal(hx, per["X"]) and torch.equal(hu, per["U"])
+    assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"])
+
+
 def test_fused_lost_handoff_is_an_error(gpu):
     """A fused-run workgroup that gives up waiting for an instance's previous step (spin bound, here one
     poll: step 1 items are drawn while step 0 still runs) makes the run an error (TRAJ_E_HANDOFF via

@@ -18,7 +18,27 @@ from trajectory_generation_amd import _lib, batch as TB  # noqa: E402
 from trajectory_generation_amd.workload import make_workload  # noqa: E402
 
 
-def main(steps=20, warm=5, B=4096, N=20, Ts=0.05, kind="spline", out=None):
+def decode(q, B, S, L, H):
+    """Work item q -> (step, rank): the fused queue order of mpc_solve.h (heavy ranks < H lead by L)."""
+    L = min(L, S) if H > 0 else 0
+    H = H if L > 0 else 0
+    P = L * H
+    step = np.empty_like(q)
+    rank = np.empty_like(q)
+    a = q < P
+    step[a], rank[a] = q[a] // max(H, 1), q[a] % max(H, 1)
+    q1 = q - P
+    full = (S - L) * B
+    b = (~a) & (q1 < full)
+    lv, r = q1[b] // B, q1[b] % B
+    step[b], rank[b] = np.where(r < H, lv + L, lv), r
+    c = (~a) & (q1 >= full)
+    q2 = q1[c] - full
+    step[c], rank[c] = (S - L) + q2 // (B - H), H + q2 % (B - H)
+    return step, rank
+
+
+def main(steps=20, warm=5, B=4096, N=20, Ts=0.05, kind="spline", out=None, lead=(1, 100)):
     dev = TB.require_gpu()
     w = make_workload(B, N, Ts, kind=kind)
     paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
@@ -31,6 +51,7 @@ def main(steps=20, warm=5, B=4096, N=20, Ts=0.05, kind="spline", out=None):
     if warm:
         TB.closed_loop_run(x, u, paths, vref, cfg, None, 0, warm, None, None, st[:warm], it[:warm])
     items = torch.zeros((steps * B, 4), dtype=torch.int64, device=dev)
+    _lib.lib().traj_debug_queue_lead(*lead)
     perm_ws = TB.workspace(B, N, dev)
     _lib.lib().traj_debug_set_item_stamps(C.c_void_p(items.data_ptr()))
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -53,7 +74,8 @@ def main(steps=20, warm=5, B=4096, N=20, Ts=0.05, kind="spline", out=None):
     wait = start - drawn
     nslots = slot.max() + 1
     q = np.arange(steps * B)
-    stp, rk = q // B, q % B
+    H = (B * lead[1]) // 1000 if warm else 0
+    stp, rk = decode(q, B, steps, lead[0], min(H, B - 1))
     inst = perm[rk]
     iters = I[stp, inst]
     res = {"launch_ms_events": ms, "span_us": span, "steps": steps, "B": B, "slots": int(nslots),

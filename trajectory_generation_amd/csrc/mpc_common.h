@@ -80,6 +80,7 @@ struct KArgs {
     int* queue;              // fused: [0] next work item, [1] error flag, [2 + b] completed steps of b
     int spin_limit;          // fused: polls of a step counter before a hand-off is declared lost
     long long* dbg_items;    // fused diagnostics: per work item q [4]: drawn, wait over, done (100 MHz), slot
+    int lead_steps, lead_h;  // fused: the heaviest lead_h ranks run lead_steps steps ahead in the queue order
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

@@ -95,7 +95,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // release / acquire on the per-instance step counter, so a slow solve delays only its instance
     // and every slot stays busy until the queue is drained.
     bool more = true;
-    int rank_of_item = 0;   // fused: rank of the current work item within its step (diagnostics)
+    int item_of_wave = 0;   // fused: the current work item (diagnostics)
     for (int step = 0; more; ++step) {
     // fused: the arguments are read through a pointer the compiler cannot see through, so nothing
     // derived from them (weights, reciprocals, per-stage predicates, address offsets) is hoisted out of
@@ -114,9 +114,34 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         const int q = s_item;
         if (q >= a.B * a.nsteps) break;
         if (a.dbg_items && threadIdx.x == 0) a.dbg_items[4 * (size_t)q] = __builtin_amdgcn_s_memrealtime();
-        step = q / a.B;
-        const int rank = q - step * a.B;
-        rank_of_item = rank;
+        // item q -> (step, rank).  Plain order: all ranks of step 0, then of step 1, ...  With a lead
+        // (a.lead_steps > 0, heavy = ranks < a.lead_h, the instances with the most ADMM iterations in the
+        // previous launch): the heavy instances' first lead steps come first, then level s holds the heavy
+        // instances' step s + lead followed by the light instances' step s -- the long chains are not held
+        // back by the level front.  Every instance's steps stay in increasing queue order, so an item only
+        // ever waits for an item drawn before it: no deadlock.
+        int rank;
+        {
+            const int Bq = a.B, S = a.nsteps;
+            const int L = (a.lead_h > 0) ? min(a.lead_steps, S) : 0, H = (L > 0) ? a.lead_h : 0;
+            const int P = L * H;
+            if (q < P) {
+                step = q / H;
+                rank = q - step * H;
+            } else {
+                const int q1 = q - P, full = (S - L) * Bq;
+                if (q1 < full) {
+                    const int lv = q1 / Bq;
+                    rank = q1 - lv * Bq;
+                    step = (rank < H) ? lv + L : lv;
+                } else {
+                    const int q2 = q1 - full, lv = (S - L) + q2 / (Bq - H);
+                    rank = H + (q2 - (lv - (S - L)) * (Bq - H));
+                    step = lv;
+                }
+            }
+        }
+        item_of_wave = q;
         b = a.perm ? a.perm[rank] : rank;
         // issue priority (s_setprio): the wave that works on a long chain gets the SIMD first -- see the
         // ADMM loop; every item starts at the default priority
@@ -1150,7 +1175,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     st_coh(m, (step == a.nsteps - 1) ? acc / a.nsteps : acc);
                 }
                 if (step == a.nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // launch span
-                if (a.dbg_items) a.dbg_items[4 * ((size_t)step * a.B + rank_of_item) + 2] = __builtin_amdgcn_s_memrealtime();
+                if (a.dbg_items) a.dbg_items[4 * (size_t)item_of_wave + 2] = __builtin_amdgcn_s_memrealtime();
                 // hand the instance to whichever workgroup takes its next step: the sc1 state stores
                 // complete (vmcnt(0)), then the step counter is stored sc1 (no L2 writeback)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
