@@ -26,9 +26,8 @@
  *     (the reference computes in numpy float64).  Shapes are given per argument.
  *   - `stream` is a hipStream_t (NULL = default stream).  Calls are asynchronous; they never
  *     copy to the host or synchronize, so they can be captured in a hipGraph.  Scratch memory is
- *     the caller's `workspace` (size from traj_mpc_workspace_bytes); the one exception is the
- *     state-bound solver (x_lo / x_hi, traj_mpc_step_batch / traj_mpc_qp_batch only), which takes
- *     its per-call scratch stream-ordered (hipMallocAsync / hipFreeAsync on `stream`).
+ *     always the caller's `workspace` (sizes from traj_mpc_workspace_bytes, plus
+ *     traj_mpc_sb_workspace_bytes for the state-bound solver); the library never allocates.
  *   - Return value: 0 on success, negative TRAJ_E_* on argument / launch errors.
  *   - Per-instance solver outcome is written to `status` (TRAJ_STATUS_*, same numbering as the
  *     CVXPY status strings listed below).  Like mpc_6stati.py:257-262, an instance whose status
@@ -44,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TRAJMPC_ABI_VERSION 1
+#define TRAJMPC_ABI_VERSION 2   /* 2: traj_mpc_qp_batch takes a workspace; traj_mpc_sb_workspace_bytes */
 
 /* error codes (return values) */
 #define TRAJ_OK 0
@@ -123,23 +122,30 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
  * closed-loop solve order (B ints, longest first) and the fused run's step queue (B + 2 ints).  Pass the same buffer to every traj_closed_loop_step of one run;
  * step t = 0 starts cold. */
 size_t traj_mpc_workspace_bytes(int B, int N);
+/* Scratch of the state-bound solver (x_lo / x_hi given with a finite side, mpc_6stati.py:208-213): B * ~20.5k
+ * doubles at N = 20.  traj_mpc_step_batch with state bounds needs traj_mpc_workspace_bytes(B, N) + this many
+ * bytes; traj_mpc_qp_batch with state bounds needs this many.  0 for B < 0 or N out of range. */
+size_t traj_mpc_sb_workspace_bytes(int B, int N);
 
 /* ---- the MPC step (mpc_6stati.py:120-275) for B independent instances ----
  * x0 [B,6], u_prev [B,2], path_ref [B,N+1,3], vref [B,N+1]  (vref None / scalar is expanded by the
  * caller, :155-160).  Outputs: u_cmd [B,2], status [B]; optional (may be NULL): objective [B],
  * X_opt [B,6,N+1], U_opt [B,2,N], iters [B] (ADMM iterations), polished [B] (1 if polish accepted).
- * workspace: device buffer of at least traj_mpc_workspace_bytes(B, N) bytes. */
+ * workspace: device buffer of at least traj_mpc_workspace_bytes(B, N) bytes (+ traj_mpc_sb_workspace_bytes(B, N)
+ * with state bounds). */
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                         const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
                         int* status, double* objective, double* X_opt, double* U_opt, int* iters, int* polished,
                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* QP half only (mpc_6stati.py:180-275) with the linearization supplied by the caller:
- * Ad [B,N,6,6], Bd [B,N,6,2], g [B,N,6].  Same outputs as traj_mpc_step_batch. */
+ * Ad [B,N,6,6], Bd [B,N,6,2], g [B,N,6].  Same outputs as traj_mpc_step_batch.  workspace: only with state
+ * bounds (>= traj_mpc_sb_workspace_bytes(B, N) bytes), otherwise may be NULL. */
 int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                       const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
                       const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
-                      double* X_opt, double* U_opt, int* iters, int* polished, void* stream);
+                      double* X_opt, double* U_opt, int* iters, int* polished, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* ---- closed loop (MPC/main.py) ----
  * Reference path per trajectory (build-defined geometry): kind[b] = 0 cubic polynomial

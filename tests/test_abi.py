@@ -81,7 +81,7 @@ def test_struct_layout_matches_c(tmp_path):
 
 
 def test_abi_version_and_strings(L):
-    assert L.traj_abi_version() == 1
+    assert L.traj_abi_version() == 2
     for code, s in _lib.STATUS_STRINGS.items():
         assert L.traj_status_string(code).decode() == s
     for rc in (_lib.TRAJ_OK, _lib.TRAJ_E_ARG, _lib.TRAJ_E_UNSUPPORTED, _lib.TRAJ_E_LAUNCH):
@@ -122,6 +122,16 @@ def test_workspace_bytes(L):
     assert L.traj_mpc_workspace_bytes(-1, 20) == 0
 
 
+def test_state_bound_workspace_bytes(L):
+    """The state-bound solver's scratch is caller-owned (mpc_general.h gen_ws_doubles per instance)."""
+    def per(N):
+        n, m = 2 * N, 10 * N
+        return n * n + m * n + 6 * (N + 1) * n + 6 * (N + 1) + 3 * n + 20 * n + 24 * m + 64
+    for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40)):
+        assert L.traj_mpc_sb_workspace_bytes(B, N) == B * per(N) * 8
+    assert L.traj_mpc_sb_workspace_bytes(-1, 20) == 0 and L.traj_mpc_sb_workspace_bytes(4, 41) == 0
+
+
 def test_argument_errors_are_reported_before_any_launch(L):
     p = _lib.default_params()
     c = _lib.default_config(20, 0.05)
@@ -148,6 +158,12 @@ def test_argument_errors_are_reported_before_any_launch(L):
     for i in range(6):
         cx.x_lo[i] = -1e3
     assert L.traj_mpc_step_batch(C.byref(p), C.byref(cx), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_OK
+    # ... with caller-owned scratch: a workspace without the state-bound part is refused before launching
+    base = L.traj_mpc_workspace_bytes(4, 20)
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cx), 4, *args, fake, base, nul) == _lib.TRAJ_E_ARG
+    assert L.traj_mpc_qp_batch(C.byref(p), C.byref(cx), 4, *([fake] * 14), nul, 0, nul) == _lib.TRAJ_E_ARG
+    assert L.traj_mpc_qp_batch(C.byref(p), C.byref(cx), 4, *([fake] * 14), fake,
+                               L.traj_mpc_sb_workspace_bytes(4, 20) - 8, nul) == _lib.TRAJ_E_ARG
     ps = _lib.Paths()
     ps.kmax, ps.kind, ps.pc = 0, 16, 16                      # never dereferenced at B = 0
     assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 0, nul, nul, nul, 0, 0, nul, nul, nul,

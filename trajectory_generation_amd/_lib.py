@@ -98,10 +98,11 @@ _SIGS = {
                                                   _V, _V]),
     "traj_lateral_error_batch": (C.c_int, [C.c_int, _V, _V, _V, _V, _V, _V, _V]),
     "traj_mpc_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "traj_mpc_sb_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
     "traj_mpc_step_batch": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.c_int, _V, _V, _V, _V,
                                       _V, _V, _V, _V, _V, _V, _V, _V, C.c_size_t, _V]),
     "traj_mpc_qp_batch": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.c_int, _V, _V, _V, _V, _V,
-                                    _V, _V, _V, _V, _V, _V, _V, _V, _V, _V]),
+                                    _V, _V, _V, _V, _V, _V, _V, _V, _V, _V, C.c_size_t, _V]),
     "traj_ref_window_batch": (C.c_int, [C.POINTER(Paths), C.c_int, C.c_int, C.c_double, _V, _V, _V, _V]),
     "traj_debug_set_stamps": (C.c_int, [_V]),
     "traj_debug_kernel_timing": (C.c_int, [C.c_int]),
@@ -161,7 +162,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.traj_abi_version() != 1:
+        if L.traj_abi_version() != 2:
             raise RuntimeError("libtrajmpc ABI version mismatch")
         _lib = L
     return _lib

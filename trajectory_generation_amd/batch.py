@@ -153,9 +153,15 @@ def _outputs(B, N, device):
 _WS = {}
 
 
-def workspace(B: int, N: int, device) -> torch.Tensor:
-    """Cached device workspace for B instances of horizon N (traj_mpc_workspace_bytes)."""
-    nbytes = int(_lib.lib().traj_mpc_workspace_bytes(int(B), int(N)))
+def _state_bounds(cfg: MpcConfig) -> bool:
+    """x_lo / x_hi given with a finite side (mpc_6stati.py:208-213): the general solver runs."""
+    return any((cfg.has_x_lo and cfg.x_lo[i] > -1e30) or (cfg.has_x_hi and cfg.x_hi[i] < 1e30) for i in range(6))
+
+
+def workspace(B: int, N: int, device, extra_bytes: int = 0) -> torch.Tensor:
+    """Cached device workspace for B instances of horizon N (traj_mpc_workspace_bytes), plus extra_bytes
+    (traj_mpc_sb_workspace_bytes: the state-bound solver's scratch, caller-owned like the rest)."""
+    nbytes = int(_lib.lib().traj_mpc_workspace_bytes(int(B), int(N))) + int(extra_bytes)
     key = (str(device), torch.cuda.current_stream(device).cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() * 8 < nbytes:
@@ -178,7 +184,8 @@ def mpc_step_batch(x0, u_prev, path_ref, vref, cfg: MpcConfig, params=None, out:
     path_ref = _dev(path_ref, (B, N + 1, 3), dev)
     vref = _dev(vref, (B, N + 1), dev)
     o = out if out is not None else _outputs(B, N, dev)
-    ws = workspace(B, N, dev)
+    sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _state_bounds(cfg) else 0
+    ws = workspace(B, N, dev, sb)
     _lib.check(_lib.lib().traj_mpc_step_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), _p(u_prev), _p(path_ref), _p(vref),
         _p(o["u_cmd"]), _p(o["status"]), _p(o["objective"]), _p(o["X_opt"]), _p(o["U_opt"]), _p(o["iters"]),
@@ -195,10 +202,12 @@ def mpc_qp_batch(x0, u_prev, path_ref, vref, Ad, Bd, g, cfg: MpcConfig, params=N
     args = [_dev(u_prev, (B, 2), dev), _dev(path_ref, (B, N + 1, 3), dev), _dev(vref, (B, N + 1), dev),
             _dev(Ad, (B, N, 6, 6), dev), _dev(Bd, (B, N, 6, 2), dev), _dev(g, (B, N, 6), dev)]
     o = _outputs(B, N, dev)
+    sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _state_bounds(cfg) else 0
+    ws = workspace(0, N, dev, sb) if sb else None
     _lib.check(_lib.lib().traj_mpc_qp_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), *[_p(a) for a in args],
         _p(o["u_cmd"]), _p(o["status"]), _p(o["objective"]), _p(o["X_opt"]), _p(o["U_opt"]), _p(o["iters"]),
-        _p(o["polished"]), _stream()), "traj_mpc_qp_batch")
+        _p(o["polished"]), _p(ws) if ws is not None else None, sb, _stream()), "traj_mpc_qp_batch")
     return o
 
 

@@ -214,16 +214,12 @@ static int check_cfg(const traj_mpc_config* c, bool allow_sb = false) {
     return TRAJ_OK;
 }
 
-// the general solver (mpc_general.h) for configurations with state bounds: per-call scratch,
-// allocated and released stream-ordered on the caller's stream
-static int launch_general(const KArgs& a, hipStream_t st) {
+// the general solver (mpc_general.h) for configurations with state bounds: its per-instance scratch is
+// the caller's (traj_mpc_sb_workspace_bytes), like every other buffer -- no allocation per call
+static int launch_general(const KArgs& a, double* gws, hipStream_t st) {
     const size_t per = gen_ws_doubles(a.c.N);
-    void* gws = nullptr;
-    if (hipMallocAsync(&gws, (size_t)a.B * per * sizeof(double), st) != hipSuccess) return TRAJ_E_LAUNCH;
-    hipLaunchKernelGGL(solve_gen_kernel, dim3(a.B), dim3(GEN_NT), 0, st, a, (double*)gws, per);
-    const bool ok = hipGetLastError() == hipSuccess;
-    if (hipFreeAsync(gws, st) != hipSuccess || !ok) return TRAJ_E_LAUNCH;
-    return TRAJ_OK;
+    hipLaunchKernelGGL(solve_gen_kernel, dim3(a.B), dim3(GEN_NT), 0, st, a, gws, per);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
 // fused run queue order: the heaviest 10 % of the instances (by the previous launch's mean ADMM
@@ -413,6 +409,11 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
+static size_t ws_base_bytes(int B, int N);
+
+// lin: the step (linearization in the library, `ws` holds its hand-off + the state-bound scratch after
+// it); !lin: the QP half (Ad / Bd / g given, `ws` is only the state-bound scratch, may be NULL without
+// state bounds)
 static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                       const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
                       const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
@@ -424,7 +425,10 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (B == 0) return TRAJ_OK;
     if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
     if (!lin && (!Ad || !Bd || !g)) return TRAJ_E_ARG;
-    if (lin && (!ws || ws_bytes < traj_mpc_workspace_bytes(B, c->N))) return TRAJ_E_ARG;
+    const bool sb = state_bounds_active(c);
+    const size_t base = lin ? ws_base_bytes(B, c->N) : 0;
+    const size_t need = base + (sb ? traj_mpc_sb_workspace_bytes(B, c->N) : 0);
+    if (need > 0 && (!ws || ws_bytes < need)) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
     a.p = *p;
@@ -441,16 +445,25 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     a.iters = iters; a.polished = polished;
     a.dbg = g_dbg;
     if (lin) launch_linearize(a, (hipStream_t)stream, false);
-    if (state_bounds_active(c)) return launch_general(a, (hipStream_t)stream);
+    if (sb) return launch_general(a, (double*)((char*)ws + base), (hipStream_t)stream);
     return launch_mpc(a, (hipStream_t)stream, lin ? 0 : 1);
+}
+
+// A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order
+// (1 int), fused-run step queue (counter, error flag, completed steps per instance); a multiple of 8
+static size_t ws_base_bytes(int B, int N) {
+    return ((size_t)B * (size_t)N * 66 + (size_t)B * 4) * sizeof(double) +
+           ((((size_t)B * 2 + 2) * sizeof(int) + 7) & ~(size_t)7);
 }
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
     if (B < 0 || N < 0) return 0;
-    // A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order
-    // (1 int), fused-run step queue (counter, error flag, completed steps per instance)
-    return ((size_t)B * (size_t)N * 66 + (size_t)B * 4) * sizeof(double) +
-           ((((size_t)B * 2 + 2) * sizeof(int) + 7) & ~(size_t)7);
+    return ws_base_bytes(B, N);
+}
+
+size_t traj_mpc_sb_workspace_bytes(int B, int N) {
+    if (B < 0 || N < 1 || N > TRAJ_MAX_N) return 0;
+    return (size_t)B * gen_ws_doubles(N) * sizeof(double);
 }
 
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
@@ -464,9 +477,10 @@ int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, 
 int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                       const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
                       const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
-                      double* X_opt, double* U_opt, int* iters, int* polished, void* stream) {
+                      double* X_opt, double* U_opt, int* iters, int* polished, void* workspace,
+                      size_t workspace_bytes, void* stream) {
     return mpc_common(p, c, B, x0, u_prev, path_ref, vref, Ad, Bd, g, u_cmd, status, objective, X_opt, U_opt, iters,
-                      polished, nullptr, 0, stream, false);
+                      polished, workspace, workspace_bytes, stream, false);
 }
 
 static bool paths_ok(const traj_paths* ps) {
