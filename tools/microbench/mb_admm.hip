@@ -63,6 +63,12 @@ __global__ __launch_bounds__(64) void admm_bench(const double* Kin, double* out,
             for (int j = 0; j < NN; j += 8) s += vb[j];
             return own ? s : 0.0;
         }
+        if (V == 7) {
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < NN; ++j) s4[j & 3] = fma(Krow[j], vb[j], s4[j & 3]);
+            return own ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0;
+        }
         double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NN; ++j) sa[j & 7] = fma(Krow[j], vb[j], sa[j & 7]);
@@ -82,6 +88,24 @@ __global__ __launch_bounds__(64) void admm_bench(const double* Kin, double* out,
     for (int it = 0; it < iters; ++it) {
         if (V == 3 || V == 5 || V == 6) {
             x = 0.5 * Kmul(x + qi) + 0.001;
+            continue;
+        }
+        if (V == 7) {
+            const double oma = 1.0 - alpha;
+            const double wb = fma(rb, zb, -yb), wr = fma(rr, zr, -yr);
+            const double wr_up = exch(wr, +2);
+            const double atw = fma(a_b, wb, fma(a_r, wr, -a_rp * wr_up));
+            const double xt = Kmul(fma(sig, x, atw - qi));
+            const double vdn = exch(xt, -2);
+            const double ztb = a_b * xt, ztr = fma(a_r, xt, -a_rm * vdn);
+            const double xn = fma(alpha, xt, oma * x);
+            const double zrb = fma(alpha, ztb, oma * zb), zrr = fma(alpha, ztr, oma * zr);
+            const double nzb = clampd(fma(rb_inv, yb, zrb), slb, sub), nzr = clampd(fma(rr_inv, yr, zrr), slr, sur);
+            yb = fma(rb, zrb - nzb, yb);
+            yr = fma(rr, zrr - nzr, yr);
+            x = xn;
+            zb = nzb;
+            zr = nzr;
             continue;
         }
         double rhs = sig * x - qi + ATw(rb * zb - yb, rr * zr - yr);
@@ -151,6 +175,11 @@ int main() {
         run<4>("everything but Kmul", nb, iters, dK, dout, dcyc, nullptr);
         run<5>("Kmul LDS part only", nb, iters, dK, dout, dcyc, nullptr);
         run<6>("Kmul FMA part only", nb, iters, dK, dout, dcyc, nullptr);
+        std::vector<double> r7;
+        run<7>("contracted + 4 chains", nb, iters, dK, dout, dcyc, &r7);
+        double md = 0;
+        for (size_t i = 0; i < r0.size(); ++i) md = std::max(md, std::abs(r0[i] - r7[i]) / (1e-300 + std::abs(r0[i])));
+        printf("  variant 7 vs 0: max rel diff %.3e\n", md);
         size_t ndiff = 0;
         for (size_t i = 0; i < r0.size(); ++i) ndiff += (r0[i] != r1[i]);
         printf("  variant 1 vs 0: %zu of %zu outputs differ\n", ndiff, r0.size());

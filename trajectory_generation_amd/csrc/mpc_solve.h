@@ -644,12 +644,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         };
         double Krow[NN];
         auto Kmul = [&](double v) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
+            // (one wave issues an f64 op about every 8 cycles, so 4 chains keep it busy; 8 cost 4 more adds)
             double vb[NN];
             lds_load_all<NN>(bcast(v), vb);
-            double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            double sa[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < NN; ++j) sa[j & 7] = fma(Krow[j], vb[j], sa[j & 7]);
-            return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
+            for (int j = 0; j < NN; ++j) sa[j & 3] = fma(Krow[j], vb[j], sa[j & 3]);
+            return own ? (sa[0] + sa[1]) + (sa[2] + sa[3]) : 0.0;
         };
         auto rho_for = [&](double l, double u, double rho) -> double {
             if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
@@ -906,19 +907,24 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 bool converged = false, refactor = false;
                 const double rb_inv = 1.0 / rb, rr_inv = 1.0 / rr;
                 int chk = c.check_interval - (iter - 1) % c.check_interval;
+                const double oma = 1.0 - alpha;
                 for (; iter <= c.max_iter; ++iter) {
+                    // OSQP's update_xz_tilde / update_x / update_z / update_y, each product-sum as an fma
+                    // (the iteration is f64-issue bound: 69 f64 ops instead of 86; the oracle keeps OSQP's
+                    // separate multiplies -- ulp-level differences, like its Cholesky vs this inverse)
                     // rhs = sig x - q + A'(rho z - y)
-                    double rhs = sig * x - qi + ATw(rb * zb - yb, rr * zr - yr);
-                    double xt = Kmul(rhs);
-                    double ztb, ztr;
-                    Ax(xt, ztb, ztr);
-                    double xn = alpha * xt + (1.0 - alpha) * x;
-                    double zrb = alpha * ztb + (1.0 - alpha) * zb;
-                    double zrr = alpha * ztr + (1.0 - alpha) * zr;
-                    double vb = zrb + rb_inv * yb, vr = zrr + rr_inv * yr;
-                    double nzb = clampd(vb, slb, sub), nzr = clampd(vr, slr, sur);
-                    yb = yb + rb * (zrb - nzb);
-                    yr = yr + rr * (zrr - nzr);
+                    const double wb = fma(rb, zb, -yb), wr = fma(rr, zr, -yr);
+                    const double wr_up = exch(wr, +2);
+                    const double atw = fma(a_b, wb, fma(a_r, wr, -(a_rp * wr_up)));
+                    double xt = Kmul(fma(sig, x, atw - qi));
+                    const double xt_dn = exch(xt, -2);
+                    const double ztb = a_b * xt, ztr = fma(a_r, xt, -(a_rm * xt_dn));
+                    double xn = fma(alpha, xt, oma * x);
+                    double zrb = fma(alpha, ztb, oma * zb);
+                    double zrr = fma(alpha, ztr, oma * zr);
+                    double nzb = clampd(fma(rb_inv, yb, zrb), slb, sub), nzr = clampd(fma(rr_inv, yr, zrr), slr, sur);
+                    yb = fma(rb, zrb - nzb, yb);
+                    yr = fma(rr, zrr - nzr, yr);
                     x = xn;
                     zb = nzb;
                     zr = nzr;
