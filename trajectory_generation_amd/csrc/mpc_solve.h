@@ -78,7 +78,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     __shared__ __attribute__((aligned(16))) double s_u[NU];
     double* const s_ex = s_u;            // exchange / broadcast buffers
     double* const s_sw = s_u + NEX;      // sweep pivot columns (16-byte aligned: NEX is even)
-    __shared__ double s_F[2 * 4 * 16 * ((NN + 15) / 16)];                    // condensing: F_k rows
+    __shared__ __attribute__((aligned(16))) double s_F[2 * 4 * 16 * ((NN + 15) / 16)];   // condensing: F_k rows; residual maxima
     __shared__ double s_red[16 * WAVES];
     __shared__ int s_flag[4];
 
@@ -657,44 +657,69 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             if (u - l < RHO_TOL) return RHO_EQ_OVER_INEQ * rho;
             return rho;
         };
-        // residuals (OSQP update_info, unscaled) : out[0..6] unscaled, [7..13] scaled norms
-        struct Res { double pr, dr, eps_p, eps_d, prs, drs, axs, zs, pxs, atys, qs; };
+        // residuals (OSQP update_info, unscaled norms; compute_rho_estimate's scaled norms).  Norms that only
+        // ever enter as a max of several are combined in the lane first, so 8 maxima cross the wave:
+        //   pr, max(|Ax|, |z|), dr, max(|Px|, |A'y|, |q|) (unscaled); prs, drs, pn, dn (scaled)
+        struct Res { double pr, dr, eps_p, eps_d, prs, drs, pn, dn; };
         auto residuals = [&](double x, double zb, double zr, double yb, double yr) -> Res {
             double axb, axr;
             Ax(x, axb, axr);
             double px = Pmul(x);
             double aty = ATw(yb, yr);
-            double v[13];
+            double v[8];
             if (own) {
                 double dres = px + qi + aty;
                 const double Dinv = 1.0 / cold(C_D), Ebinv = 1.0 / cold(C_EB), Erinv = 1.0 / cold(C_ER);
                 v[0] = fmax(fabs(Ebinv * (axb - zb)), fabs(Erinv * (axr - zr)));   // prim res
-                v[1] = fmax(fabs(Ebinv * axb), fabs(Erinv * axr));
-                v[2] = fmax(fabs(Ebinv * zb), fabs(Erinv * zr));
-                v[3] = fabs(Dinv * dres) * csinv;
-                v[4] = fabs(Dinv * px) * csinv;
-                v[5] = fabs(Dinv * aty) * csinv;
-                v[6] = fabs(Dinv * qi) * csinv;
-                v[7] = fmax(fabs(axb - zb), fabs(axr - zr));
-                v[8] = fabs(dres);
-                v[9] = fmax(fabs(axb), fabs(axr));
-                v[10] = fmax(fabs(zb), fabs(zr));
-                v[11] = fabs(px);
-                v[12] = fmax(fabs(aty), fabs(qi));
+                v[1] = fmax(fmax(fabs(Ebinv * axb), fabs(Erinv * axr)), fmax(fabs(Ebinv * zb), fabs(Erinv * zr)));
+                v[2] = fabs(Dinv * dres) * csinv;
+                v[3] = fmax(fabs(Dinv * px) * csinv, fmax(fabs(Dinv * aty) * csinv, fabs(Dinv * qi) * csinv));
+                v[4] = fmax(fabs(axb - zb), fabs(axr - zr));
+                v[5] = fabs(dres);
+                v[6] = fmax(fmax(fabs(axb), fabs(axr)), fmax(fabs(zb), fabs(zr)));
+                v[7] = fmax(fabs(px), fmax(fabs(aty), fabs(qi)));
             } else {
-                for (int i = 0; i < 13; ++i) v[i] = 0.0;
+                for (int i = 0; i < 8; ++i) v[i] = 0.0;
             }
-            double atys_only = own ? fabs(aty) : 0.0, qs_only = own ? fabs(qi) : 0.0;
-            block_max(v);
-            double w2[2] = {atys_only, qs_only};
-            block_max(w2);
+            if constexpr (WAVES == 1) {
+                // one wave: transposed through LDS (s_F, free during the solve).  Lane 8 i + p takes the max
+                // of value i over lanes [p NN/8, (p+1) NN/8), three DPP steps join the 8 parts, and the 8
+                // maxima come back as one broadcast read -- ~30 instructions where 8 butterflies take ~180.
+                // NaN anywhere in a value makes that maximum NaN (as wave_max_dpp).
+                static_assert(NN % 8 == 0 && 8 * NN <= 2 * 4 * 16 * ((NN + 15) / 16), "s_F too small");
+                constexpr int PL = NN / 8;
+                bool nan[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) nan[i] = __ballot(v[i] != v[i]) != 0;
+                if (t < NN) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) s_F[i * NN + t] = v[i];
+                }
+                __syncthreads();
+                const double* src = s_F + (t >> 3) * NN + (t & 7) * PL;
+                double m = src[0];
+#pragma unroll
+                for (int k = 1; k < PL; ++k) m = fmax(m, src[k]);
+                m = fmax(m, dpp_d<0xB1>(m));    // lane ^ 1
+                m = fmax(m, dpp_d<0x4E>(m));    // lane ^ 2
+                m = fmax(m, dpp_d<0x141>(m));   // half-row mirror: quads of one 8-lane group
+                __syncthreads();
+                if ((t & 7) == 0) s_F[t >> 3] = m;
+                __syncthreads();
+                double mv[8];
+                lds_load_all<8>(s_F, mv);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = nan[i] ? __builtin_nan("") : mv[i];
+                __syncthreads();
+            } else {
+                block_max(v);
+            }
             Res r;
             r.pr = v[0];
-            r.eps_p = c.eps_abs + c.eps_rel * fmax(v[1], v[2]);
-            r.dr = v[3];
-            r.eps_d = c.eps_abs + c.eps_rel * fmax(v[4], fmax(v[5], v[6]));
-            r.prs = v[7]; r.drs = v[8]; r.axs = v[9]; r.zs = v[10]; r.pxs = v[11];
-            r.atys = w2[0]; r.qs = w2[1];
+            r.eps_p = c.eps_abs + c.eps_rel * v[1];
+            r.dr = v[2];
+            r.eps_d = c.eps_abs + c.eps_rel * v[3];
+            r.prs = v[4]; r.drs = v[5]; r.pn = v[6]; r.dn = v[7];
             return r;
         };
 
@@ -720,7 +745,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             }
         }
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
-        Res r = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        Res r = {0, 0, 0, 0, 0, 0, 0, 0};
         int rounds = 0, ps = 0, actb = 0, actr = 0;
         double escale = 1.0;
         const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
@@ -941,9 +966,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                         ++n_res;
                         if (r.pr <= escale * r.eps_p && r.dr <= escale * r.eps_d) { converged = true; break; }
                         if (c.adaptive_rho) {
-                            double pn = fmax(r.axs, r.zs);
-                            double dn = fmax(r.pxs, fmax(r.atys, r.qs));
-                            double est = rho * sqrt((r.prs / (pn + DIV_TOL)) / (r.drs / (dn + DIV_TOL) + DIV_TOL));
+                            double est = rho * sqrt((r.prs / (r.pn + DIV_TOL)) / (r.drs / (r.dn + DIV_TOL) + DIV_TOL));
                             est = fmin(fmax(est, RHO_MIN), RHO_MAX);
                             if (est > rho * c.adaptive_rho_tol || est < rho / c.adaptive_rho_tol) {
                                 rho = est;
