@@ -1,0 +1,167 @@
+// Microbenchmark: the one-wave receiver-lane sweep of solve_kernel (mpc_solve.h, NN = 40): K^{-1} in place
+// by the symmetric sweep operator, one pivot column broadcast through LDS per pivot.  Variants:
+//   0: as in the kernel (each pivot reads its row, then 1/d, then the FMAs)
+//   1: the next pivot's d read right after this pivot's column is published and its 1/d formed under
+//      this pivot's FMAs (off the critical chain)
+//   2: as 1, and the whole next pivot row read before this pivot's FMAs (double-buffered row)
+// Prints cycles per sweep (median wave) at 1 and 2 waves per SIMD and checks the variants are
+// bit-identical.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "../../trajectory_generation_amd/csrc/mpc_common.h"
+
+using namespace tgmpc;
+constexpr int NN = 40;
+
+template <int V>
+__global__ __launch_bounds__(64) void sweep_bench(const double* Kin, double* out, long long* cyc, int reps) {
+    __shared__ __attribute__((aligned(16))) double s_sw[2 * (2 * NN + 2)];
+    const int t = threadIdx.x;
+    double Krow[NN];
+    long long total = 0;
+    bool ok = true;
+    double acc = 0.0;
+    for (int rep = 0; rep < reps; ++rep) {
+#pragma unroll
+        for (int j = 0; j < NN; ++j) Krow[j] = t < NN ? Kin[t * NN + j] + 1e-3 * rep : 0.0;
+        __syncthreads();
+        const long long t0 = __builtin_amdgcn_s_memtime();
+        constexpr int SB = 2 * NN + 2;
+        constexpr int SPARE = 64 - NN;
+        int rho = t < NN ? t : -1;
+        if (t < NN) {
+            s_sw[t] = Krow[0];
+            s_sw[t + NN] = Krow[0];
+        }
+        double dinv_n = 0.0;
+        if (V >= 1) {
+            __syncthreads();
+            const double d0 = s_sw[0];
+            ok = ok && (d0 > 0.0);
+            dinv_n = rcp_nr(d0);
+        }
+        double2 prn[NN / 2];
+        if (V == 2) {
+            const double2* p2 = reinterpret_cast<const double2*>(s_sw);
+#pragma unroll
+            for (int i = 0; i < NN / 2; ++i) prn[i] = p2[i];
+        }
+#pragma nounroll
+        for (int pv = 0; pv < NN; ++pv) {
+            if (NN > SPARE && pv == SPARE) {
+                if (t < SPARE) {
+#pragma unroll
+                    for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
+                }
+            }
+            __syncthreads();
+            const int o = pv & 1;
+            double2 pr[NN / 2];
+            if (V == 2) {
+#pragma unroll
+                for (int i = 0; i < NN / 2; ++i) pr[i] = prn[i];
+            } else {
+                const double* prow = s_sw + o * SB + o + pv;
+                const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
+#pragma unroll
+                for (int i = 0; i < NN / 2; ++i) pr[i] = prow2[i];
+            }
+            double dinv;
+            if (V == 0) {
+                const double d = pr[0].x;
+                ok = ok && (d > 0.0);
+                dinv = rcp_nr(d);
+            } else {
+                dinv = dinv_n;
+            }
+            const int rl = pv < SPARE ? NN + pv : pv - SPARE;
+            const bool recv = (t == rl);
+            const double fd = Krow[0] * dinv;
+            const double be = recv ? dinv : -fd;
+            const double k0 = recv ? -dinv : fd;
+            rho = recv ? pv : ((t == pv) ? -1 : rho);
+            const double n0 = fma3(be, pr[0].y, Krow[1]);
+            double* nb = s_sw + (o ^ 1) * SB + (o ^ 1);
+            if (rho >= 0) {
+                nb[rho] = n0;
+                nb[rho + NN] = n0;
+            }
+            if (V >= 1 && pv + 1 < NN) {
+                __syncthreads();   // one wave: orders the LDS accesses (no barrier instruction)
+                if (V == 2) {
+                    const double2* q2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(nb + pv + 1, 16));
+#pragma unroll
+                    for (int i = 0; i < NN / 2; ++i) prn[i] = q2[i];
+                    const double dn = prn[0].x;
+                    ok = ok && (dn > 0.0);
+                    dinv_n = rcp_nr(dn);
+                } else {
+                    const double dn = nb[pv + 1];
+                    ok = ok && (dn > 0.0);
+                    dinv_n = rcp_nr(dn);
+                }
+            }
+#pragma unroll
+            for (int j = 2; j < NN; ++j) Krow[j - 1] = fma3(be, (j & 1) ? pr[j >> 1].y : pr[j >> 1].x, Krow[j]);
+            Krow[0] = n0;
+            Krow[NN - 1] = k0;
+        }
+        const int src = ((t + NN) & 63) << 2;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) {
+            const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(Krow[j]));
+            const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(Krow[j]));
+            Krow[j] = __hiloint2double(hi, lo);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const long long t1 = __builtin_amdgcn_s_memtime();
+        total += t1 - t0;
+#pragma unroll
+        for (int j = 0; j < NN; ++j) acc += Krow[j] * (1 + j);
+    }
+    out[blockIdx.x * 64 + t] = ok ? acc : -1.0;
+    if (t == 0) cyc[blockIdx.x] = total;
+}
+
+template <int V>
+static double run(const char* name, int nblk, int reps, const double* dK, double* dout, long long* dcyc,
+                  std::vector<double>& res) {
+    hipLaunchKernelGGL(sweep_bench<V>, dim3(nblk), dim3(64), 0, 0, dK, dout, dcyc, reps);
+    (void)hipDeviceSynchronize();
+    std::vector<long long> c(nblk);
+    (void)hipMemcpy(c.data(), dcyc, nblk * sizeof(long long), hipMemcpyDeviceToHost);
+    res.resize((size_t)nblk * 64);
+    (void)hipMemcpy(res.data(), dout, res.size() * 8, hipMemcpyDeviceToHost);
+    std::sort(c.begin(), c.end());
+    const double cps = (double)c[nblk / 2] / reps;
+    printf("%-40s blocks %5d: %8.0f cycles/sweep (median wave), %.0f per pivot\n", name, nblk, cps, cps / NN);
+    return cps;
+}
+
+int main() {
+    double *dK, *dout;
+    long long* dcyc;
+    std::vector<double> K(NN * NN);
+    for (int i = 0; i < NN; ++i)
+        for (int j = 0; j < NN; ++j) K[i * NN + j] = (i == j ? 2.0 + 0.1 * i : 0.05 / (1 + std::abs(i - j)));
+    (void)hipMalloc(&dK, K.size() * 8);
+    (void)hipMalloc(&dout, 8192 * 64 * 8);
+    (void)hipMalloc(&dcyc, 8192 * 8);
+    (void)hipMemcpy(dK, K.data(), K.size() * 8, hipMemcpyHostToDevice);
+    const int reps = 50;
+    for (int nb : {1024, 2048}) {
+        std::vector<double> r0, r1, r2;
+        run<0>("sweep as in the kernel", nb, reps, dK, dout, dcyc, r0);
+        run<1>("next 1/d under this pivot's FMAs", nb, reps, dK, dout, dcyc, r1);
+        run<2>("+ next row read before the FMAs", nb, reps, dK, dout, dcyc, r2);
+        size_t d1 = 0, d2 = 0;
+        for (size_t i = 0; i < r0.size(); ++i) { d1 += r0[i] != r1[i]; d2 += r0[i] != r2[i]; }
+        printf("  outputs differing from variant 0: v1 %zu, v2 %zu of %zu (ok flag %s)\n", d1, d2, r0.size(),
+               r0[0] > 0 ? "set" : "CLEARED");
+    }
+    return 0;
+}
