@@ -418,6 +418,13 @@ def main():
                          "valu_insts_per_step": ij["valu_insts_per_step"],
                          "valu_issue_frac": ij["valu_insts_per_step"] * 4 * value / world / (SIMDS * CLOCK_HZ),
                          "source": os.path.relpath(args.issue_json, HERE)}
+                if "f64_valu_insts_per_step" in ij:
+                    # SIMD VALU busy time on CDNA4 (MI355X_MICROARCH.md, per-instruction constants): a wave64
+                    # f64 instruction holds the 16-lane f64 pipe 4 cycles, any other VALU instruction the
+                    # 32-wide SIMD 2 cycles
+                    f64i = ij["f64_valu_insts_per_step"]
+                    issue["simd_valu_busy_frac"] = ((f64i * 4 + (ij["valu_insts_per_step"] - f64i) * 2) * value / world
+                                                    / (SIMDS * CLOCK_HZ))
         except (OSError, ValueError, KeyError):
             issue = None
     out = {
