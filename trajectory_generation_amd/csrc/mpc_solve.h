@@ -618,7 +618,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             const int rt = t * NN - (t * (t - 1)) / 2 - t;
 #pragma unroll
             for (int j = 0; j < NN; ++j)
-                if (j >= t) s_P[rt + j] = own ? Prow[j] : 0.0;
+                if (j >= t) s_P[rt + j] = own ? Prow[j] : ((j == t) ? 1.0 : 0.0);   // identity on padding rows
         }
         __syncthreads();
         stamp(5, __builtin_amdgcn_s_memtime());
@@ -767,17 +767,37 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             {
                 const double kr_up = exch(kr, +2);
                 const double dii = ks + kb * a_b * a_b + kr * a_r * a_r + kr_up * a_rp * a_rp;
-                const double dm = -kr * a_r * a_rm;        // (t, t-2)
-                const double dp = -kr_up * cold(C_ARUP) * a_rp;  // (t, t+2)
+                // (t, t+2); by symmetry also the (t+2, t) entry: lane t+2's -kr a_r a_rm is the same product
+                // of the same values (kr_up = kr(t+2), cold(C_ARUP) = a_r(t+2), a_rp = Er(t+2) D(t) = a_rm(t+2))
+                const double dp = -kr_up * cold(C_ARUP) * a_rp;
+                // The band goes into the packed P in LDS (each own lane adds its diagonal and its (t, t+2)
+                // entry), every lane reads its row as it stands -- no per-entry selects -- and the two entries
+                // are restored.  Padding rows n..NN-1 hold the identity in s_P; lanes >= NN hold exact zero rows
+                // (the receivers of the one-wave sweep below).
                 const int tt = opaque_t();
+                const int pdg = paddr(tt, tt), psp = paddr(tt + 2, tt);
+                const bool has_sp = own && (t + 2 < n);
+                double o_dg = 0.0, o_sp = 0.0;
+                if (own) {
+                    o_dg = s_P[pdg];
+                    s_P[pdg] = o_dg + dii;
+                    if (has_sp) {
+                        o_sp = s_P[psp];
+                        s_P[psp] = o_sp + dp;
+                    }
+                }
+                __syncthreads();
+                if (WAVES > 1 || t < NN) {
 #pragma unroll
-                for (int j = 0; j < NN; ++j) {
-                    double v = own ? s_P[paddr(j, tt)] : 0.0;
-                    v += (j == tt) ? (own ? dii : 1.0) : 0.0;    // identity padding for rows n..NN-1
-                    v += (j == tt - 2) ? dm : 0.0;
-                    v += (j == tt + 2) ? dp : 0.0;
-                    // lanes >= NN hold exact zero rows (the receivers of the one-wave sweep below)
-                    Krow[j] = (WAVES == 1 && t >= NN) ? 0.0 : v;
+                    for (int j = 0; j < NN; ++j) Krow[j] = (WAVES == 1 || t < NN) ? s_P[paddr(j, tt)] : 0.0;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
+                }
+                __syncthreads();
+                if (own) {
+                    s_P[pdg] = o_dg;
+                    if (has_sp) s_P[psp] = o_sp;
                 }
             }
             // ---- sweep: Krow <- row t of K^{-1} (symmetric sweep operator, NN pivots) ----
