@@ -76,4 +76,5 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
 
 if __name__ == "__main__":
     main(polish_mode=int(sys.argv[1]) if len(sys.argv) > 1 else 0, warm=int(sys.argv[2]) if len(sys.argv) > 2 else 5,
-         fused=int(sys.argv[3]) if len(sys.argv) > 3 else 0)
+         fused=int(sys.argv[3]) if len(sys.argv) > 3 else 0, N=int(sys.argv[4]) if len(sys.argv) > 4 else 20,
+         kind=sys.argv[5] if len(sys.argv) > 5 else "spline")

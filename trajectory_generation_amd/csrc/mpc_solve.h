@@ -645,11 +645,26 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         double Krow[NN];
         auto Kmul = [&](double v) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
             // (one wave issues an f64 op about every 8 cycles, so 4 chains keep it busy; 8 cost 4 more adds)
-            double vb[NN];
-            lds_load_all<NN>(bcast(v), vb);
             double sa[4] = {0.0, 0.0, 0.0, 0.0};
+            const double* vbuf = bcast(v);
+            if constexpr (NN <= 64) {
+                double vb[NN];
+                lds_load_all<NN>(vbuf, vb);
 #pragma unroll
-            for (int j = 0; j < NN; ++j) sa[j & 3] = fma(Krow[j], vb[j], sa[j & 3]);
+                for (int j = 0; j < NN; ++j) sa[j & 3] = fma(Krow[j], vb[j], sa[j & 3]);
+            } else {
+                // NN = 80: the whole vector in flight (160 VGPRs beside the 160 of Krow) spills inside the
+                // ADMM loop; 16 values at a time, same FMA order
+                constexpr int CH = 16;
+                static_assert(NN % CH == 0, "chunked broadcast");
+#pragma unroll
+                for (int c0 = 0; c0 < NN; c0 += CH) {
+                    double vb[CH];
+                    lds_load_all<CH>(vbuf + c0, vb);
+#pragma unroll
+                    for (int j = 0; j < CH; ++j) sa[(c0 + j) & 3] = fma(Krow[c0 + j], vb[j], sa[(c0 + j) & 3]);
+                }
+            }
             return own ? (sa[0] + sa[1]) + (sa[2] + sa[3]) : 0.0;
         };
         auto rho_for = [&](double l, double u, double rho) -> double {
