@@ -73,7 +73,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     __shared__ double s_sc[(NM + 1) * 2];
     // one region, two lives: the solve's exchange / broadcast buffers and sweep pivot columns, or (fused,
     // during block_linearize) the Jacobian's tire evaluations [NM][TJ]
-    constexpr int NEX = 6 * NN, NSW = 2 * (2 * NN + 2);
+    // exchange buffers: 4 rotating slots of NN (+ 2 more for the two-wave condensing's 2 x 3 NN), and for
+    // two waves 3 fixed slots (4, 5, 6) for the ADMM loop's three exchanges, so no rotating index lives
+    // across that loop (at NN = 80 it was spilled and reloaded from scratch in every exchange)
+    constexpr int NEX = (WAVES > 1) ? (4 * NN + 3 * NT > 6 * NN ? 4 * NN + 3 * NT : 6 * NN) : 6 * NN;
+    constexpr int NSW = 2 * (2 * NN + 2);
     constexpr int NU = (NEX + NSW > TJ * NM) ? NEX + NSW : TJ * NM;
     __shared__ __attribute__((aligned(16))) double s_u[NU];
     double* const s_ex = s_u;            // exchange / broadcast buffers
@@ -222,6 +226,23 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         __syncthreads();
         return buf;
     };
+    // two waves, ADMM loop: the same exchange / broadcast through a fixed slot (see NEX).  The exchange
+    // slots are NT wide and every lane writes: a non-own lane's value is never read by an own lane (reads
+    // stop at s < n), and what non-own lanes receive only ever reaches non-own lanes -- so no lane flag
+    // has to stay live across the loop
+    auto exch_at = [&](double v, int delta, int slot) -> double {
+        double* buf = s_ex + 4 * NN + (slot - 4) * NT;
+        buf[t] = v;
+        __syncthreads();
+        const int s = t + delta;
+        return (s >= 0 && s < n) ? buf[s] : 0.0;
+    };
+    auto bcast_at = [&](double v, int slot) -> double* {
+        double* buf = s_ex + 4 * NN + (slot - 4) * NT;
+        if (own) buf[t] = v;
+        __syncthreads();
+        return buf;
+    };
     auto block_max = [&](auto& v) {                   // in-place max over the block (uniform result)
         constexpr int V = sizeof(v) / sizeof(double);
         if (WAVES == 1) {
@@ -258,7 +279,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
     // exchange buffers start at zero: entries >= n are the zero padding the unguarded
     // register loops over the full capacity NN rely on
-    for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;
+    for (int i = t; i < NEX; i += NT) s_ex[i] = 0.0;
     for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
     if (FUSED) {   // the state the instance's previous step published (sc1, see st_coh)
         if (t < 6) s_x0[t] = ld_coh(a.x_state + 6 * b + t);
@@ -314,7 +335,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_F, s_u, s_big, s_big + 36 * N, s_big + 48 * N,
                             a.dbg ? a.dbg + (size_t)b * 32 : nullptr);
         for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
-        for (int i = t; i < 6 * NN; i += NT) s_ex[i] = 0.0;   // s_u held the tire evaluations
+        for (int i = t; i < NEX; i += NT) s_ex[i] = 0.0;   // s_u held the tire evaluations
     } else if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
         // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
         // at once (one L2/MALL latency, no VGPRs); the three blocks are contiguous in s_big as double2
@@ -643,10 +664,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
         };
         double Krow[NN];
-        auto Kmul = [&](double v) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
+        auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
             // (one wave issues an f64 op about every 8 cycles, so 4 chains keep it busy; 8 cost 4 more adds)
             double sa[4] = {0.0, 0.0, 0.0, 0.0};
-            const double* vbuf = bcast(v);
+            const double* vbuf = (slot >= 0) ? bcast_at(v, slot) : bcast(v);
             if constexpr (NN <= 64) {
                 double vb[NN];
                 lds_load_all<NN>(vbuf, vb);
@@ -974,10 +995,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     // separate multiplies -- ulp-level differences, like its Cholesky vs this inverse)
                     // rhs = sig x - q + A'(rho z - y)
                     const double wb = fma(rb, zb, -yb), wr = fma(rr, zr, -yr);
-                    const double wr_up = exch(wr, +2);
+                    const double wr_up = (WAVES > 1) ? exch_at(wr, +2, 4) : exch(wr, +2);
                     const double atw = fma(a_b, wb, fma(a_r, wr, -(a_rp * wr_up)));
-                    double xt = Kmul(fma(sig, x, atw - qi));
-                    const double xt_dn = exch(xt, -2);
+                    double xt = Kmul(fma(sig, x, atw - qi), WAVES > 1 ? 5 : -1);
+                    const double xt_dn = (WAVES > 1) ? exch_at(xt, -2, 6) : exch(xt, -2);
                     const double ztb = a_b * xt, ztr = fma(a_r, xt, -(a_rm * xt_dn));
                     double xn = fma(alpha, xt, oma * x);
                     double zrb = fma(alpha, ztb, oma * zb);
