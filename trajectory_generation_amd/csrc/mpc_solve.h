@@ -508,12 +508,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                         if (i <= j && j < NN) s_P[i * NN - (i * (i - 1)) / 2 + (j - i)] = acc[ti][reg];
                     }
             __syncthreads();
-            const int tt = opaque_t();
-#pragma unroll
-            for (int j = 0; j < NN; ++j) Prow[j] = own ? s_P[paddr(j, tt)] : 0.0;
         }
     }
-    stamp(19, __builtin_amdgcn_s_memtime());
     // input penalties U'RU and dU'Rd dU (dU_0 = U_0 - u_prev)
     double Rs[4], Rds[4];
     Rs[0] = c.R[0]; Rs[3] = c.R[3]; Rs[1] = Rs[2] = 0.5 * (c.R[1] + c.R[2]);
@@ -521,8 +517,30 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // this thread's rows of Rs / Rds (selects, not a dynamic index: keeps them in registers)
     const double Rs0 = ch ? Rs[2] : Rs[0], Rs1 = ch ? Rs[3] : Rs[1];
     const double Rd0 = ch ? Rds[2] : Rds[0], Rd1 = ch ? Rds[3] : Rds[1];
-    if (own) {
-        const double dmul = (kk < N - 1) ? 2.0 : 1.0;
+    const double dmul = (kk < N - 1) ? 2.0 : 1.0;
+    if constexpr (WAVES == 1) {
+        // One wave: the penalty band goes into the packed P in LDS before the rows are read back.  Row t's
+        // upper-triangle entries that get a term: the diagonal; for channel 0 its stage partner (t + 1) and
+        // the next stage's two inputs (t + 2, t + 3); for channel 1 the next stage's (t + 1, t + 2).  Each
+        // lower entry is the upper entry of another row with the same term bit for bit (Rs[1] = Rs[2],
+        // Rds[1] = Rds[2]), so adding each entry once gives the rows the per-entry loop gave.
+        if (own) {
+            const int rb0 = t * NN - (t * (t - 1)) / 2 - t;   // packed row t: P(t, j) at rb0 + j
+            s_P[rb0 + t] = s_P[rb0 + t] + (2.0 * (ch ? Rs1 : Rs0) + 2.0 * (ch ? Rd1 : Rd0) * dmul);
+            if (ch == 0) {
+                s_P[rb0 + t + 1] = s_P[rb0 + t + 1] + (2.0 * Rs1 + 2.0 * Rd1 * dmul);
+                if (t + 2 < n) s_P[rb0 + t + 2] = s_P[rb0 + t + 2] + -2.0 * Rd0;
+                if (t + 3 < n) s_P[rb0 + t + 3] = s_P[rb0 + t + 3] + -2.0 * Rd1;
+            } else {
+                if (t + 1 < n) s_P[rb0 + t + 1] = s_P[rb0 + t + 1] + -2.0 * Rd0;
+                if (t + 2 < n) s_P[rb0 + t + 2] = s_P[rb0 + t + 2] + -2.0 * Rd1;
+            }
+        }
+        __syncthreads();
+        const int tt = opaque_t();
+#pragma unroll
+        for (int j = 0; j < NN; ++j) Prow[j] = own ? s_P[paddr(j, tt)] : 0.0;
+    } else if (own) {
 #pragma unroll
         for (int j = 0; j < NN; ++j) {
             const int kj = j >> 1;
@@ -531,8 +549,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             add = (j < n && (kj == kk - 1 || kj == kk + 1)) ? -2.0 * rd : add;
             Prow[j] += add;
         }
-        if (kk == 0) qi -= 2.0 * (Rd0 * s_up[0] + Rd1 * s_up[1]);
     }
+    stamp(19, __builtin_amdgcn_s_memtime());
+    if (own && kk == 0) qi -= 2.0 * (Rd0 * s_up[0] + Rd1 * s_up[1]);
 
     // constraint rows owned by t: box (U_t) and rate (U_t - U_{t-2}, or U_0 - u_prev)
     double lb = ch ? c.u_lo[1] : c.u_lo[0], ub = ch ? c.u_hi[1] : c.u_hi[0];
