@@ -242,7 +242,7 @@ static int g_lead_steps = TGMPC_LEAD_STEPS, g_lead_permille = TGMPC_LEAD_PERMILL
 static std::vector<hipEvent_t> g_ev;
 static int g_ev_used = 0;
 static inline void stamp(int k, hipStream_t st) {
-    if ((size_t)(5 * g_ev_used + k) < g_ev.size()) hipEventRecord(g_ev[5 * g_ev_used + k], st);
+    if ((size_t)(5 * g_ev_used + k) < g_ev.size()) (void)hipEventRecord(g_ev[5 * g_ev_used + k], st);
 }
 
 static inline unsigned nblk(int B, int bs) { return (unsigned)((B + bs - 1) / bs); }
@@ -285,7 +285,7 @@ int traj_debug_spin_limit(int polls) {
 }
 
 int traj_debug_kernel_timing(int max_steps) {
-    for (hipEvent_t e : g_ev) hipEventDestroy(e);
+    for (hipEvent_t e : g_ev) (void)hipEventDestroy(e);
     g_ev.clear();
     g_ev_used = 0;
     if (max_steps < 0) return TRAJ_E_ARG;
