@@ -595,9 +595,15 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         // so the column norms of the scaled P are cs * cn with cn = max_j |Prow_j|, tracked in the
         // scaling pass itself (one pass over the row per iteration instead of four).
         double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0;
-        double cn = 0.0;
+        // (maxima in 4 interleaved partials: max is exact, so this is the sequential result with a quarter
+        // of its dependent chain)
+        double cn;
+        {
+            double c4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int j = 0; j < NN; ++j) cn = fmax(cn, fabs(Prow[j]));
+            for (int j = 0; j < NN; ++j) c4[j & 3] = fmax(c4[j & 3], fabs(Prow[j]));
+            cn = fmax(fmax(c4[0], c4[1]), fmax(c4[2], c4[3]));
+        }
         for (int it = 0; it < c.scaling_iters; ++it) {
             double Er_up = exch(Er, +2);     // E of rate row t+2
             double D_dn = exch(D, -2);       // D of variable t-2
@@ -609,13 +615,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
             double Dv[NN];
             lds_load_all<NN>(bcast(Dt), Dv);   // all reads in flight at once (not one wait per read)
-            cn = 0.0;
+            double c4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int j = 0; j < NN; ++j) {
                 const double v = Prow[j] * (Dt * Dv[j]);
                 Prow[j] = v;
-                cn = fmax(cn, fabs(v));
+                c4[j & 3] = fmax(c4[j & 3], fabs(v));
             }
+            cn = fmax(fmax(c4[0], c4[1]), fmax(c4[2], c4[3]));
             qi *= Dt;
             D *= Dt;
             Eb *= Etb;
