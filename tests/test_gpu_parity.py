@@ -611,3 +611,36 @@ def test_config3_hard_states_vs_fixture(gpu):
     assert cert.sum() >= 16
     du = np.abs(ox["U_opt"][cert] - g["U_opt"][keep][ok][cert]).max()
     assert du <= 1e-4, du
+
+
+def test_divergent_dataset_trajectory_step_gate(gpu, oracle_lib):
+    """configs[3]'s rare divergent trajectory (id 1854 of the bench workload leaves the
+    stable regime at dt = 0.05, vx < 0 from step 9, solver errors from ~step 70 in this build's realization):
+    whatever realization a build produces, every step of the GPU closed loop, re-solved from the GPU's own
+    state by the step entry point and by the oracle (cold start), has the oracle's status, and u agrees where
+    both polished (1e-6) or both stopped unpolished at the same ADMM iteration (1e-3)."""
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T = 20, 0.05, 75
+    w = make_workload(4, N, Ts, kind="spline", seed=0, id_offset=1852)   # ids 1852..1855 (per-id seeds)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts)
+    res = {k: v.cpu().numpy() for k, v in TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg).items()}
+    vr = np.tile(w["vref"], (4, 1))
+    n_cmp = 0
+    for t in range(T):
+        xt = res["X"][:, t]
+        ut = res["U"][:, t - 1] if t > 0 else w["u0"]
+        if not np.isfinite(xt).all():
+            break
+        prt = TB.ref_window_batch(paths, xt[:, 0], vr, N, Ts).cpu().numpy()
+        g = {k: v.cpu().numpy() for k, v in TB.mpc_step_batch(xt, ut, prt, vr, cfg).items()}
+        ro = oracle_lib.mpc_step_batch(xt, ut, prt, vr, oracle_lib.cfg(N=N, Ts=Ts))
+        assert np.array_equal(g["status"], ro["status"]), (t, g["status"], ro["status"])
+        ok = g["status"] <= 1
+        both = ok & (g["polished"] > 0) & (ro["polished"] > 0)
+        du = np.abs(g["u_cmd"] - ro["u_cmd"]).max(axis=1)
+        assert du[both].max(initial=0.0) <= 1e-6, (t, du)
+        eq = ok & (g["polished"] == 0) & (ro["polished"] == 0) & (g["iters"] == ro["iters"])
+        assert du[eq].max(initial=0.0) <= 1e-3, (t, du)
+        n_cmp += int(both.sum() + eq.sum())
+    assert n_cmp >= 200
