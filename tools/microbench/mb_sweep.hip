@@ -91,7 +91,8 @@ __global__ __launch_bounds__(64) void sweep_bench(const double* Kin, double* out
                 nb[rho + NN] = n0;
             }
             if (V >= 1 && pv + 1 < NN) {
-                __syncthreads();   // one wave: orders the LDS accesses (no barrier instruction)
+                if (V == 3) asm volatile("" ::: "memory");   // one wave: LDS executes its DS ops in order
+                else __syncthreads();
                 if (V == 2) {
                     const double2* q2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(nb + pv + 1, 16));
 #pragma unroll
@@ -158,8 +159,11 @@ int main() {
         run<0>("sweep as in the kernel", nb, reps, dK, dout, dcyc, r0);
         run<1>("next 1/d under this pivot's FMAs", nb, reps, dK, dout, dcyc, r1);
         run<2>("+ next row read before the FMAs", nb, reps, dK, dout, dcyc, r2);
-        size_t d1 = 0, d2 = 0;
-        for (size_t i = 0; i < r0.size(); ++i) { d1 += r0[i] != r1[i]; d2 += r0[i] != r2[i]; }
+        std::vector<double> r3;
+        run<3>("next 1/d, no wait after the publish", nb, reps, dK, dout, dcyc, r3);
+        size_t d1 = 0, d2 = 0, d3 = 0;
+        for (size_t i = 0; i < r0.size(); ++i) { d1 += r0[i] != r1[i]; d2 += r0[i] != r2[i]; d3 += r0[i] != r3[i]; }
+        printf("  variant 3 differs in %zu outputs\n", d3);
         printf("  outputs differing from variant 0: v1 %zu, v2 %zu of %zu (ok flag %s)\n", d1, d2, r0.size(),
                r0[0] > 0 ? "set" : "CLEARED");
     }
