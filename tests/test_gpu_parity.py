@@ -384,6 +384,35 @@ def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
         assert torch.equal(per[k], fus2[k]), k
 
 
+def _same(a, b):
+    """Equal bit for bit, NaN == NaN (a diverged trajectory's history holds NaN in both runs)."""
+    return bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) if a.is_floating_point() else torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,warm,mode", [(20, 1, 0), (18, 1, 0), (20, 0, 1)])
+def test_fused_three_waves_bit_identical(gpu, N, warm, mode):
+    """The 3-waves-per-SIMD fused instance (capacity 40: 168 VGPRs, compact LDS image; chosen for runs of
+    TRAJ_FUSED_W3_MIN_STEPS or more) equals the 2-wave instance and the per-step launches bit for bit; N = 18
+    leaves padding rows in the capacity-40 kernel."""
+    from trajectory_generation_amd import _lib
+    from trajectory_generation_amd.workload import make_workload
+    Ts, T, B = 0.05, 200, 96
+    w = make_workload(B, N, Ts, kind="spline", seed=11)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=warm, polish_mode=mode)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    runs = {}
+    try:
+        for wv in (2, 3, 0):   # forced 2, forced 3, by launch length (200 steps: 3)
+            _lib.check(_lib.lib().traj_debug_fused_waves(wv), "traj_debug_fused_waves")
+            runs[wv] = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    finally:
+        _lib.lib().traj_debug_fused_waves(0)
+    for wv, r in runs.items():
+        for k in ("X", "U", "status", "iters"):
+            assert _same(per[k], r[k]), (wv, k)
+
+
 @pytest.mark.parametrize("lead", [(0, 0), (3, 500), (1, 999)])
 def test_fused_queue_lead_bit_identical(gpu, lead):
     """The fused run's queue order (heavy instances ahead of the level front, traj_debug_queue_lead) moves

@@ -109,6 +109,7 @@ _SIGS = {
     "traj_debug_fused_grid": (C.c_int, [C.c_int]),
     "traj_debug_spin_limit": (C.c_int, [C.c_int]),
     "traj_debug_queue_lead": (C.c_int, [C.c_int, C.c_int]),
+    "traj_debug_fused_waves": (C.c_int, [C.c_int]),
     "traj_debug_set_item_stamps": (C.c_int, [_V]),
     "traj_closed_loop_check": (C.c_int, [_V, C.c_size_t, C.c_int, C.c_int, _V]),
     "traj_dataset_write_csv": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_double, _V, _V, _V, _V,
@@ -159,6 +160,8 @@ def lib():
                                "or __graft_entry__.build() (no CPU fallback exists)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("TRAJMPC_LIB") and name.startswith("traj_debug_") and not hasattr(L, name):
+                continue   # an older variant build (experiments) may lack a newer diagnostic entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -81,6 +81,7 @@ struct KArgs {
     int spin_limit;          // fused: polls of a step counter before a hand-off is declared lost
     long long* dbg_items;    // fused diagnostics: per work item q [4]: drawn, wait over, done (100 MHz), slot
     int lead_steps, lead_h;  // fused: the heaviest lead_h ranks run lead_steps steps ahead in the queue order
+    int wps;                 // fused: waves per SIMD of the kernel instance to launch (2, or 3 where built)
 };
 
 __device__ __forceinline__ double limit_scaling(double v) {

@@ -1,6 +1,6 @@
 // mpc_inst.hip -- one translation unit per horizon capacity (compiled with -DTGMPC_NN=<NN>), so
 // the fully unrolled instantiations of the MPC kernels build in parallel.
-#include "mpc_solve.h"
+#include "mpc_launch.h"
 
 #ifndef TGMPC_NN
 #error "compile with -DTGMPC_NN=<capacity>"
@@ -11,32 +11,20 @@
 
 namespace tgmpc {
 
+#if TGMPC_NN == 40
+int launch_fused_w3_40(const KArgs& a, hipStream_t st);   // mpc_inst_w3.hip
+#endif
+
 // mode 0: MPC step, 1: QP only (A/B/g given), 2: closed-loop step (the linearization launches are
 // issued by the caller, trajmpc.hip), 3: fused closed loop of a.nsteps steps (linearization inside)
 int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
     constexpr int NN = TGMPC_NN;
     dim3 grid(a.B), sblock(((NN + 63) / 64) * 64);
     if (mode == 3) {
-        // fused: one workgroup per resident slot (occupancy x CUs), each running its instances
-        // step by step; at most TRAJ_FUSED_MAX_PER_WG instances per workgroup
-        static int slots_per_cu[64] = {0};
-        static int cus[64] = {0};
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -3;
-        if (!slots_per_cu[dev]) {
-            int nb = 0, ncu = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, solve_kernel<NN, true, true>, (int)sblock.x, 0) !=
-                    hipSuccess ||
-                hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                return -3;
-            slots_per_cu[dev] = nb < 1 ? 1 : (nb > 8 ? 8 : nb);
-            cus[dev] = ncu < 1 ? 1 : ncu;
-        }
-        int G = a.fused_grid > 0 ? a.fused_grid : slots_per_cu[dev] * cus[dev];
-        if (G > a.B) G = a.B;
-        const int minG = (a.B + TRAJ_FUSED_MAX_PER_WG - 1) / TRAJ_FUSED_MAX_PER_WG;
-        if (G < minG) G = minG;
-        hipLaunchKernelGGL((solve_kernel<NN, true, true>), dim3(G), sblock, 0, st, a);
+#if TGMPC_NN == 40
+        if (a.wps == 3) return launch_fused_w3_40(a, st);
+#endif
+        return launch_fused<NN, 2>(a, st);
     }
     else if (mode == 2) hipLaunchKernelGGL((solve_kernel<NN, true>), grid, sblock, 0, st, a);
     else hipLaunchKernelGGL((solve_kernel<NN, false>), grid, sblock, 0, st, a);

@@ -246,8 +246,7 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 
 // In-workgroup linearization for the fused closed loop (traj_closed_loop_run): rollout_kernel's
 // and jac_kernel's arithmetic for ONE instance and NT threads, with A_k, B_k, g_k written to LDS in the
-// solve kernel's staging layout.  xs / us: the state and input (LDS); xf: scratch [N][12] (LDS);
-// tj: scratch [N][TJ] (LDS) for the Jacobian's tire / sincos evaluations.  Ends with a barrier.
+// stage records the solve kernel's condensing reads.  xs / us: the state and input (LDS).  Ends with a barrier.
 //
 // The rollout is a serial chain: per stage, atan2 -> atan -> sincos on three lanes.  The Jacobian
 // columns of stage k need the same chain at perturbed copies of x_k, known as soon as x_k is: lanes
@@ -262,10 +261,17 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 // stage per lane) then forms f at each perturbed point with f_parts and the difference quotients:
 // the values state_column / cheap_columns compute (jac_kernel), bit for bit.
 constexpr int TJ = 24;
+// Layout: one record of LREC doubles per stage, rec + LREC k = [A_k 36 | B_k 12 | g_k 6] on exit.  While
+// the stage is being formed the same record holds its scratch: the tire / sincos evaluations at [0, TJ) and
+// the rollout's (x_k, f_k) at [TJ, TJ + 12).  Only the lane that assembles stage k reads them, and it writes
+// the outputs after its reads, so no stage's scratch is overwritten before it is consumed.
+constexpr int LREC = 54;
+static_assert(TJ + 12 <= 36, "a stage's scratch must lie inside its record's A_k part");
 template <int NT>
 __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N, double Ts, const double* xs,
-                                                const double* us, double* xf, double* tj, double* A, double* Bm,
-                                                double* g, long long* dbg = nullptr) {
+                                                const double* us, double* rec, long long* dbg = nullptr) {
+    double* const tj = rec;                // [k]: rec + LREC k + [0, TJ)
+    double* const xf = rec + TJ;           // [k]: rec + LREC k + TJ + [0, 12)
     auto mark = [&](int i) { if (dbg && t == 0) dbg[i] = __builtin_amdgcn_s_memtime(); };
     const double eps = 1e-5;
     if (t < 64) {
@@ -297,8 +303,8 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
             const double z = tire ? Ct * atan(Bt * alpha) : (t == 2 ? phi : phi + pz);
             double sz, cz;
             sincos(z, &sz, &cz);
-            if (t >= 3 && t <= 21) tj[TJ * k + t] = sz;
-            if (t >= 19 && t <= 21) tj[TJ * k + t - 19] = cz;
+            if (t >= 3 && t <= 21) tj[LREC * k + t] = sz;
+            if (t >= 19 && t <= 21) tj[LREC * k + t - 19] = cz;
             const double Fy_f = p.Df * readlane_d(sz, 0), Fy_r = p.Dr * readlane_d(sz, 1);
             const double sphi = readlane_d(sz, 2), cphi = readlane_d(cz, 2);
             const double Frx = (p.Cm1 - p.Cm2 * vx) * u0 - p.Cr0 - p.Cr2 * (vx * vx);
@@ -311,8 +317,8 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
             f[5] = (1.0 / p.Iz) * (Fy_f * p.lf * cd - Fy_r * p.lr);
             if (t == 0)
                 for (int i = 0; i < 6; ++i) {
-                    xf[12 * k + i] = x[i];
-                    xf[12 * k + 6 + i] = f[i];
+                    xf[LREC * k + i] = x[i];
+                    xf[LREC * k + 6 + i] = f[i];
                 }
             for (int i = 0; i < 6; ++i) x[i] = x[i] + Ts * f[i];
         }
@@ -328,9 +334,9 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
     sincos(de + eps, &sdp, &cdp);
     sincos(de - eps, &sdm, &cdm);
     for (int k = t; k < N; k += NT) {
-        const double* T = tj + TJ * k;
+        const double* T = tj + LREC * k;
         double xb[6], fk[6];
-        for (int i = 0; i < 6; ++i) { xb[i] = xf[12 * k + i]; fk[i] = xf[12 * k + 6 + i]; }
+        for (int i = 0; i < 6; ++i) { xb[i] = xf[LREC * k + i]; fk[i] = xf[LREC * k + 6 + i]; }
         const double vx0 = xb[3] + 0.0, vy0 = xb[4] + 0.0, om0 = xb[5] + 0.0;
         const double sphi = T[21], cphi = T[2];
         const double Ff0 = p.Df * T[3], Fr0 = p.Dr * T[4], Fx0 = long_force(p, vx0, d);
@@ -381,9 +387,10 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
         }
         double gk[6];
         g_stage(Ak, Bk, xb, fk, d, de, Ts, gk);
-        for (int i = 0; i < 36; ++i) A[36 * k + i] = Ak[i];
-        for (int i = 0; i < 12; ++i) Bm[12 * k + i] = Bk[i];
-        for (int r = 0; r < 6; ++r) g[6 * k + r] = gk[r];
+        double* const o = rec + LREC * k;   // (after every read of this stage's scratch)
+        for (int i = 0; i < 36; ++i) o[i] = Ak[i];
+        for (int i = 0; i < 12; ++i) o[36 + i] = Bk[i];
+        for (int r = 0; r < 6; ++r) o[48 + r] = gk[r];
     }
     __syncthreads();
 }

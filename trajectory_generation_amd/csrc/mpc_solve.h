@@ -28,8 +28,18 @@
 #ifndef TGMPC_PRIO_LAG
 #define TGMPC_PRIO_LAG 0       // fused run: items of instances >= this many steps behind the draw front run at priority 3
 #endif
+#ifndef TGMPC_PRIO_HEAVY
+#define TGMPC_PRIO_HEAVY 0     // fused run: items of the heavy (lead) ranks run at priority 3 from their start
+#endif
 #ifndef TGMPC_PRIO_RANK
 #define TGMPC_PRIO_RANK 0      // fused run: heaviest ranks (per mille of B) whose items run at priority 2
+#endif
+
+#ifndef TGMPC_KCH
+#define TGMPC_KCH 8            // CMP: broadcast values per chunk of the ADMM mat-vec
+#endif
+#ifndef TGMPC_PCH
+#define TGMPC_PCH 4            // CMP: pivot-row double2 per chunk of the sweep
 #endif
 
 namespace tgmpc {
@@ -51,39 +61,72 @@ __device__ __forceinline__ double ld_coh(const double* p) {
 // NN = capacity in QP variables (>= 2N); CLOSED = closed-loop step (window from the state, plant
 // update, history).  A_k, B_k, g_k are read from a.Ad / a.Bd / a.gd ([B,N,36], [B,N,12], [B,N,6]).
 // =====================================================================================
-template <int NN, bool CLOSED, bool FUSED = false>
-__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(NN <= 64 ? 2 : 1))) void solve_kernel(const KArgs a0) {
+// DIAG: the diagnostics (a.dbg stamps, a.dbg_items timeline) are compiled in; the fused launch uses the
+// DIAG = false instance unless a diagnostic buffer is set (their counters cost registers in every phase)
+// WPS: waves per SIMD the register allocation is held to (fused one-wave kernels: 2, or 3 -- 168 VGPRs, the
+// compact LDS image; mpc_inst_w3.hip).
+template <int NN, bool CLOSED, bool FUSED = false, bool DIAG = true, int WPS = 2>
+// (capacity 64: the row of K^-1 and its broadcast vector alone are 256 VGPRs -- one wave per SIMD)
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(NN <= 40 ? WPS : 1))) void solve_kernel(const KArgs a0) {
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
     constexpr int NP = NN * (NN + 1) / 2;
 
-    __shared__ double s_pref[3 * (NM + 1)];
-    __shared__ double s_vref[NM + 1];
+    // CMP (fused, one wave): the compact LDS image -- at most 13 KB, so that 12 workgroups (3 waves per
+    // SIMD) fit a CU's 160 KB.  One wave's LDS operations complete in program order, so buffers whose
+    // lives do not overlap share one region (see s_scr).
+    constexpr bool CMP = FUSED && WAVES == 1;
+    // LEAN (the 3-wave instance): values parked in / re-formed from LDS around the factorization, a rolled P v
+    // -- register savings the 2-wave instance does without (same arithmetic, same results)
+    constexpr bool LEAN = CMP && WPS >= 3;
+    __shared__ double s_pref0[CMP ? 2 : 3 * (NM + 1)];
+    __shared__ double s_vref0[CMP ? 2 : NM + 1];
     __shared__ double s_x0[6], s_up[2];
     __shared__ int s_item;
-    // one region, two lives: A_k, B_k, g_k of every stage staged for the condensing, then (once P
-    // is formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values
+    // one region, two lives: A_k, B_k, g_k of every stage staged for the condensing (fused: stage records
+    // [A_k 36 | B_k 12 | g_k 6], which also hold block_linearize's scratch for the stage), then (once P is
+    // formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values (rows of CS; CMP:
+    // NN wide: the spare lanes read the next row's values, or lane CS-1's pair, and never use them)
+    constexpr int CS = (WAVES == 1) ? NN : NT;
+    constexpr int NCOLD = 11 * CS;   // 5 single rows + 3 pair rows (see the cold values below)
     constexpr int NLIN = 54 * NM;
-    constexpr int NBIG = (NP + 8 * NT > NLIN) ? NP + 8 * NT : NLIN;
+    constexpr int NBIG0 = (NP + NCOLD > NLIN) ? NP + NCOLD : NLIN;
+    constexpr int NDMA = FUSED ? 0 : 2 * NT * ((27 * NM + NT - 1) / NT);   // the LDS-DMA staging tail (below)
+    constexpr int NBIG = NBIG0 > NDMA ? NBIG0 : NDMA;
     __shared__ __attribute__((aligned(16))) double s_big[NBIG];
     double* const s_P = s_big;
     double* const s_cold = s_big + NP;
-    __shared__ double s_xh[(NM + 1) * 6];
-    __shared__ double s_sc[(NM + 1) * 2];
-    // one region, two lives: the solve's exchange / broadcast buffers and sweep pivot columns, or (fused,
-    // during block_linearize) the Jacobian's tire evaluations [NM][TJ]
+    __shared__ double s_xh[CLOSED ? 6 : (NM + 1) * 6];   // X_opt by the linear model (not in the closed loop)
+    __shared__ double s_sc0[CMP ? 2 : (NM + 1) * 2];
     // exchange buffers: 4 rotating slots of NN (+ 2 more for the two-wave condensing's 2 x 3 NN), and for
     // two waves 3 fixed slots (4, 5, 6) for the ADMM loop's three exchanges, so no rotating index lives
     // across that loop (at NN = 80 it was spilled and reloaded from scratch in every exchange)
-    constexpr int NEX = (WAVES > 1) ? (4 * NN + 3 * NT > 6 * NN ? 4 * NN + 3 * NT : 6 * NN) : 6 * NN;
+    constexpr int NEX = (WAVES > 1) ? (4 * NN + 3 * NT > 6 * NN ? 4 * NN + 3 * NT : 6 * NN) : (CMP ? 4 * NN : 6 * NN);
     constexpr int NSW = 2 * (2 * NN + 2);
-    constexpr int NU = (NEX + NSW > TJ * NM) ? NEX + NSW : TJ * NM;
+    constexpr int FS = 16 * ((NN + 15) / 16);
+    constexpr int NFS = (CMP ? 1 : 2) * 4 * FS;          // condensing F_k rows: slots of 4 x FS
+    // CMP: one scratch region for the exchange / broadcast slots (ADMM, Ruiz, polish), the sweep's pivot
+    // columns (factorization), the condensing's F rows and the residual transposition (8 NN + 8) -- each
+    // phase leaves nothing there the next one reads.  Otherwise: exchange + sweep buffers, and s_F apart.
+    constexpr int NSCR0 = (NEX > NSW) ? NEX : NSW;
+    constexpr int NWIN = CMP ? 6 * (NM + 1) : 0;   // CMP: the window and sin/cos(phi*) after the F slot
+    constexpr int NSCR1 = (NFS + NWIN > 8 * NN) ? NFS + NWIN : 8 * NN;
+    // CMP: the ADMM iterate (x, z, y: 5 rows of NN) is parked past the pivot columns during each K build + sweep
+    constexpr int NSTASH = LEAN ? ((NSW + 1) & ~1) + 5 * NN : 0;
+    constexpr int NU0 = CMP ? ((NSCR0 > NSCR1) ? NSCR0 : NSCR1) : NEX + NSW;
+    constexpr int NU = NU0 > NSTASH ? NU0 : NSTASH;
     __shared__ __attribute__((aligned(16))) double s_u[NU];
-    double* const s_ex = s_u;            // exchange / broadcast buffers
-    double* const s_sw = s_u + NEX;      // sweep pivot columns (16-byte aligned: NEX is even)
-    __shared__ __attribute__((aligned(16))) double s_F[2 * 4 * 16 * ((NN + 15) / 16)];   // condensing: F_k rows; residual maxima
-    __shared__ double s_red[16 * WAVES];
+    double* const s_ex = s_u;                     // exchange / broadcast buffers
+    double* const s_sw = CMP ? s_u : s_u + NEX;   // sweep pivot columns (16-byte aligned: NEX is even)
+    __shared__ __attribute__((aligned(16))) double s_F0[CMP ? 2 : NFS];
+    double* const s_F = CMP ? s_u : s_F0;         // condensing: F_k rows; residual maxima
+    // the reference window (X*, Y*, phi*) and vref of the stages, sin / cos(phi*_k): CMP keeps them in s_u past
+    // the F slot -- read only up to the condensing (the closed loop reports no X_opt or objective)
+    double* const s_pref = CMP ? s_u + NFS : s_pref0;
+    double* const s_vref = CMP ? s_u + NFS + 3 * (NM + 1) : s_vref0;
+    double* const s_sc = CMP ? s_u + NFS + 4 * (NM + 1) : s_sc0;
+    __shared__ double s_red[WAVES > 1 ? 16 * WAVES : 2];
     __shared__ int s_flag[4];
 
     // Fused closed loop (traj_closed_loop_run): nsteps steps of this instance in one launch -- the
@@ -110,6 +153,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     KArgsPtr ap = FUSED ? (KArgsPtr)__builtin_amdgcn_kernarg_segment_ptr() : (KArgsPtr) nullptr;
     if constexpr (FUSED) asm volatile("" : "+s"(ap));
     const KArgs& a = FUSED ? *(const KArgs*)ap : a0;
+    long long* const dbg = DIAG ? a.dbg : nullptr;               // diagnostics, or null
+    long long* const dbg_items = DIAG ? a.dbg_items : nullptr;
     int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
     if constexpr (FUSED) {
         __syncthreads();
@@ -117,7 +162,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         __syncthreads();
         const int q = s_item;
         if (q >= a.B * a.nsteps) break;
-        if (a.dbg_items && threadIdx.x == 0) a.dbg_items[4 * (size_t)q] = __builtin_amdgcn_s_memrealtime();
+        if (dbg_items && threadIdx.x == 0) dbg_items[4 * (size_t)q] = __builtin_amdgcn_s_memrealtime();
         // item q -> (step, rank).  Plain order: all ranks of step 0, then of step 1, ...  With a lead
         // (a.lead_steps > 0, heavy = ranks < a.lead_h, the instances with the most ADMM iterations in the
         // previous launch): the heavy instances' first lead steps come first, then level s holds the heavy
@@ -153,6 +198,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #if TGMPC_PRIO_RANK > 0
         if (a.perm && rank * 1000 < a.B * TGMPC_PRIO_RANK) __builtin_amdgcn_s_setprio(2);
 #endif
+#if TGMPC_PRIO_HEAVY
+        // the heavy instances (the queue's lead set: the most ADMM iterations in the previous launch) are the
+        // launch's critical chains -- their items issue first for the whole item
+        if (a.perm && rank < a.lead_h) __builtin_amdgcn_s_setprio(3);
+#endif
         if (threadIdx.x == 0 && step > 0) {
             int spins = 0;
             while (__hip_atomic_load(&a.queue[2 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < step) {
@@ -172,17 +222,17 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         if (s_item / a.B - step >= TGMPC_PRIO_LAG) __builtin_amdgcn_s_setprio(3);
 #endif
         __syncthreads();
-        if (a.dbg_items && threadIdx.x == 0) {   // diagnostics: item timeline (traj_debug_set_item_stamps)
-            a.dbg_items[4 * (size_t)q + 1] = __builtin_amdgcn_s_memrealtime();
-            a.dbg_items[4 * (size_t)q + 3] = blockIdx.x;
+        if (dbg_items && threadIdx.x == 0) {   // diagnostics: item timeline (traj_debug_set_item_stamps)
+            dbg_items[4 * (size_t)q + 1] = __builtin_amdgcn_s_memrealtime();
+            dbg_items[4 * (size_t)q + 3] = blockIdx.x;
         }
-        if (a.dbg && threadIdx.x == 0 && step == 0) {   // diagnostics: start, HW_ID, XCC_ID
+        if (dbg && threadIdx.x == 0 && step == 0) {   // diagnostics: start, HW_ID, XCC_ID
             unsigned hw, xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            a.dbg[(size_t)b * 32 + 22] = __builtin_amdgcn_s_memrealtime();
-            a.dbg[(size_t)b * 32 + 24] = hw;
-            a.dbg[(size_t)b * 32 + 25] = xcc;
+            dbg[(size_t)b * 32 + 22] = __builtin_amdgcn_s_memrealtime();
+            dbg[(size_t)b * 32 + 24] = hw;
+            dbg[(size_t)b * 32 + 25] = xcc;
         }
     } else {
         more = false;
@@ -199,7 +249,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     const int kk = t >> 1, ch = t & 1;  // stage and channel of variable t
     int xb = 0;                         // rotating exchange buffer
     auto stamp = [&](int i, long long v) {
-        if (a.dbg && t == 0) a.dbg[(size_t)b * 32 + i] = v;
+        if (dbg && t == 0) dbg[(size_t)b * 32 + i] = v;
     };
     stamp(0, __builtin_amdgcn_s_memtime());
 
@@ -220,9 +270,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         }
     };
     auto bcast = [&](double v) -> double* {            // publish v_t for all, returns buffer
-        double* buf = s_ex + (xb & 3) * NN;
-        xb++;
-        if (own) buf[t] = v;
+        // (CMP: one slot -- the previous broadcast's reads precede this write in the wave's LDS order)
+        double* buf = CMP ? s_ex : s_ex + (xb & 3) * NN;
+        if constexpr (!CMP) xb++;
+        // (every lane < NN writes: entries n .. NN-1 are the zero padding the register loops over NN read,
+        // and in the compact image another phase may have used the slot)
+        if (t < NN) buf[t] = own ? v : 0.0;
         __syncthreads();
         return buf;
     };
@@ -280,7 +333,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // exchange buffers start at zero: entries >= n are the zero padding the unguarded
     // register loops over the full capacity NN rely on
     for (int i = t; i < NEX; i += NT) s_ex[i] = 0.0;
-    for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
+    for (int i = t; i < NFS; i += NT) s_F[i] = 0.0;
     if (FUSED) {   // the state the instance's previous step published (sc1, see st_coh)
         if (t < 6) s_x0[t] = ld_coh(a.x_state + 6 * b + t);
         if (t < 2) s_up[t] = ld_coh(a.u_state + 2 * b + t);
@@ -330,13 +383,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     stamp(2, __builtin_amdgcn_s_memrealtime());   // 100 MHz wall clock (comparable across XCDs)
     // ---- 3. condensed QP (:180-250) --------------------------------------------------
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
-    if (fused) {
-        // s_F (the condensing's F rows) is the rollout record's scratch here; zeroed again after
-        block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_F, s_u, s_big, s_big + 36 * N, s_big + 48 * N,
-                            a.dbg ? a.dbg + (size_t)b * 32 : nullptr);
-        for (int i = t; i < 2 * 4 * 16 * ((NN + 15) / 16); i += NT) s_F[i] = 0.0;
-        for (int i = t; i < NEX; i += NT) s_ex[i] = 0.0;   // s_u held the tire evaluations
-    } else if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
+    if constexpr (FUSED) {
+        // A_k, B_k, g_k as stage records (LREC doubles each) in s_big
+        block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_big, dbg ? dbg + (size_t)b * 32 : nullptr);
+    } else {
+    if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
         // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
         // at once (one L2/MALL latency, no VGPRs); the three blocks are contiguous in s_big as double2
         // [A 18N | B 6N | g 3N].  Chunk r lands at s_big2[r NT + lane]; lanes past the end re-load
@@ -357,10 +408,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         for (int i = t; i < 12 * N; i += NT) s_big[36 * N + i] = gB[i];
         for (int i = t; i < 6 * N; i += NT) s_big[48 * N + i] = gg[i];
     }
+    }
     stamp(16, __builtin_amdgcn_s_memtime());
+    // stage k's A_k at cA + RA k, B_k at cB + RB k, g_k at cg + RG k (fused: block_linearize's stage records)
+    constexpr int RA = FUSED ? LREC : 36, RB = FUSED ? LREC : 12, RG = FUSED ? LREC : 6;
     const double* const cA = s_big;
-    const double* const cB = s_big + 36 * N;
-    const double* const cg = s_big + 48 * N;
+    const double* const cB = s_big + (FUSED ? 36 : 36 * N);
+    const double* const cg = s_big + (FUSED ? 48 : 48 * N);
     // sin / cos of phi*_k for every stage (lane-parallel)
     for (int k = t; k <= N; k += NT) {
         double sk, ck;
@@ -382,11 +436,20 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // Both give an exactly symmetric P (each unordered pair is formed once / by a commutative product).
     double Prow[NN];
     double qi = 0.0;
+    // (a fresh copy of the lane index per use, so that nothing derived from it is kept live across phases;
+    // lanes >= NN read in-range LDS words for their masked-off rows)
     auto opaque_t = [&]() -> int {
         int r;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t < NN ? t : 0));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(t));
         return r;
     };
+    // Row tt of the packed upper triangle, entry j: P(j, tt) = s_P[C_j + tt] for j < tt (C_j uniform) and
+    // P(tt, j) = s_P[rt + j] for j >= tt (rt = prow_base(tt), the lane's row start).
+    auto prow_entry = [&](int j, int tt, int rt) -> double {
+        const int cj = j * NN - (j * (j - 1)) / 2 - j;
+        return s_P[(j < tt) ? tt + cj : rt + j];
+    };
+    auto prow_base = [&](int tt) -> int { return tt * NN - (tt * (tt - 1)) / 2 - tt; };
     auto paddr = [&](int j, int tt) -> int {   // packed upper triangle: P(i, j), i <= j
         return (j < tt) ? (j * NN - (j * (j - 1)) / 2 - j + tt) : (tt * NN - (tt * (tt - 1)) / 2 - tt + j);
     };
@@ -416,13 +479,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         }
         const int mr = (t >> 4) & 3, mc = t & 15;   // MFMA operand slot of this lane: k-row, column
         for (int k = 0; k < N; ++k) {
-            const double* Ak = cA + 36 * k;
+            const double* Ak = cA + RA * k;
             if constexpr (!FREE_LANE) {
                 // free response xh_{k+1} = A_k xh_k + g_k (uniform)
                 double xn[6];
 #pragma unroll
                 for (int r = 0; r < 6; ++r) {
-                    double v = cg[6 * k + r];
+                    double v = cg[RG * k + r];
 #pragma unroll
                     for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], xh[cc], v);
                     xn[r] = v;
@@ -439,10 +502,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 double Gn[6];
 #pragma unroll
                 for (int r = 0; r < 6; ++r) {
-                    double v = fl ? cg[6 * k + r] : 0.0;
+                    double v = fl ? cg[RG * k + r] : 0.0;
 #pragma unroll
                     for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], G[cc], v);
-                    const double bv = cB[12 * k + 2 * r + ch];
+                    const double bv = cB[RB * k + 2 * r + ch];
                     Gn[r] = prop ? v : (enter ? bv : G[r]);
                 }
 #pragma unroll
@@ -461,7 +524,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
             qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
             if constexpr (WAVES == 1) {
-                double* fb = s_F + (k & 1) * 4 * FS;    // 2 rotating slots; row 3 and columns >= n stay 0
+                double* fb = s_F + (CMP ? 0 : (k & 1) * 4 * FS);   // 2 rotating slots (CMP: 1); row 3 and columns >= n stay 0
 #ifdef TGMPC_EXP_NO_FSYNC
                 double opv[NB];
 #pragma unroll
@@ -613,14 +676,22 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
             double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
             double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
-            double Dv[NN];
-            lds_load_all<NN>(bcast(Dt), Dv);   // all reads in flight at once (not one wait per read)
+            // the broadcast D read in chunks of RCH, each chunk's reads in flight at once (CMP: 8, so that the
+            // row of P and the chunk fit the 3-wave register budget; otherwise the whole vector)
+            const double* dvb = bcast(Dt);
             double c4[4] = {0.0, 0.0, 0.0, 0.0};
+            constexpr int RCH = CMP ? 8 : NN;
+            static_assert(NN % RCH == 0, "chunked broadcast");
 #pragma unroll
-            for (int j = 0; j < NN; ++j) {
-                const double v = Prow[j] * (Dt * Dv[j]);
-                Prow[j] = v;
-                c4[j & 3] = fmax(c4[j & 3], fabs(v));
+            for (int c0 = 0; c0 < NN; c0 += RCH) {
+                double Dv[RCH];
+                lds_load_all<RCH>(dvb + c0, Dv);
+#pragma unroll
+                for (int j = 0; j < RCH; ++j) {
+                    const double v = Prow[c0 + j] * (Dt * Dv[j]);
+                    Prow[c0 + j] = v;
+                    c4[(c0 + j) & 3] = fmax(c4[(c0 + j) & 3], fabs(v));
+                }
             }
             cn = fmax(fmax(c4[0], c4[1]), fmax(c4[2], c4[3]));
             qi *= Dt;
@@ -638,27 +709,52 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #pragma unroll
         for (int j = 0; j < NN; ++j) Prow[j] *= cs;
         qi *= cs;
-        const double csinv = 1.0 / cs;   // uniform
+        const double csinv = uniformize(1.0 / cs);   // uniform (held in SGPRs, not in VGPRs)
         const double D_dn = exch(D, -2), Er_up = exch(Er, +2);
-        const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
-        // scaled bounds
-        const double slb = (lb > -INFTY) ? lb * Eb : -INFTY, sub = (ub < INFTY) ? ub * Eb : INFTY;
-        const double slr = (lr > -INFTY) ? lr * Er : -INFTY, sur = (ur < INFTY) ? ur * Er : INFTY;
+        // (a_rp(t) = Er(t+2) D(t) is a_rm(t+2) bit for bit: where it is needed it is taken from lane t+2 --
+        // exch(a_rm, +2), or the product a_rm w formed on lane t+2 -- instead of living in a register)
+        double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0;   // (CMP: re-formed, see reload)
+        (void)Er_up;
         // Cold per-lane values go to LDS and are re-read (volatile: never hoisted into registers)
-        // where needed -- residual checks, the K build, polish -- keeping the ADMM loop's live set
-        // down to the inverse row + ~16 doubles.
-        enum { C_D = 0, C_EB, C_ER, C_LB, C_UB, C_LR, C_UR, C_ARUP };
+        // where needed -- residual checks, the K build, polish, the ADMM loop's clamps -- keeping the ADMM
+        // loop's live set down to the inverse row + ~12 doubles.  Single rows: D, E_box, E_rate, a_r(t+2), q.
+        // Pair rows (lane t: [2t], [2t+1], one ds_read_b128): (1 / rho_box, 1 / rho_rate) and the scaled
+        // bounds (lb, ub), (lr, ur) of the box and rate rows.
+        enum { C_D = 0, C_EB, C_ER, C_ARUP, C_Q };
+        enum { P_RHOI = 0, P_BB, P_BR };
+        typedef double dpair __attribute__((ext_vector_type(2)));
+        typedef __attribute__((address_space(3))) volatile dpair* LdsVD2;
+        const int tc = t < CS ? t : CS - 1;
+        auto pair = [&](int i) -> dpair { return ((LdsVD2)(s_cold + 5 * CS))[i * CS + tc]; };
+        auto set_pair = [&](int i, double x0, double x1) {
+            if (t < CS) ((LdsVD2)(s_cold + 5 * CS))[i * CS + t] = dpair{x0, x1};
+        };
         {
+            // scaled bounds
+            const double slb = (lb > -INFTY) ? lb * Eb : -INFTY, sub = (ub < INFTY) ? ub * Eb : INFTY;
+            const double slr = (lr > -INFTY) ? lr * Er : -INFTY, sur = (ur < INFTY) ? ur * Er : INFTY;
             const double a_r_up0 = exch(a_r, +2);
-            double* cw = s_cold + t;
-            cw[C_D * NT] = D; cw[C_EB * NT] = Eb; cw[C_ER * NT] = Er;
-            cw[C_LB * NT] = lb; cw[C_UB * NT] = ub; cw[C_LR * NT] = lr; cw[C_UR * NT] = ur;
-            cw[C_ARUP * NT] = a_r_up0;
+            if (t < CS) {   // (rows of CS: lanes >= CS read the next row's values, never use them)
+                double* cw = s_cold + t;
+                cw[C_D * CS] = D; cw[C_EB * CS] = Eb; cw[C_ER * CS] = Er;
+                cw[C_ARUP * CS] = a_r_up0;
+                cw[C_Q * CS] = qi;
+            }
+            set_pair(P_BB, slb, sub);
+            set_pair(P_BR, slr, sur);
         }
         // (an LDS-typed volatile pointer: ds_read with a 32-bit address -- a generic volatile pointer
         // becomes a flat load with a 64-bit address per value)
         typedef __attribute__((address_space(3))) volatile double* LdsVD;
-        auto cold = [&](int i) -> double { return ((LdsVD)s_cold)[i * NT + t]; };
+        auto cold = [&](int i) -> double { return ((LdsVD)s_cold)[i * CS + t]; };
+        // the unscaled bounds of rows t (as formed above from the configuration; exact-mode certificate)
+        auto raw_bounds = [&](double& lb_, double& ub_, double& lr_, double& ur_) {
+            lb_ = ch ? c.u_lo[1] : c.u_lo[0];
+            ub_ = ch ? c.u_hi[1] : c.u_hi[0];
+            lr_ = ch ? c.du_lo[1] : c.du_lo[0];
+            ur_ = ch ? c.du_hi[1] : c.du_hi[0];
+            if (kk == 0) { lr_ += s_up[ch]; ur_ += s_up[ch]; }
+        };
         // scaled P to LDS (row stride PS)
         // packed upper triangle: P(i, j), i <= j, at i*NN - i(i-1)/2 + (j - i); rows >= n are zero
         if (t < NN) {
@@ -678,15 +774,27 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         };
         // A' w for w = (wb, wr)
         auto ATw = [&](double wb, double wr) -> double {
-            double wr_up = exch(wr, +2);
-            return a_b * wb + a_r * wr - a_rp * wr_up;
+            const double rp_up = exch(a_rm * wr, +2);   // a_rp(t) wr(t+2), formed on lane t+2
+            return a_b * wb + a_r * wr - rp_up;
         };
         auto Pmul = [&](double v) -> double {  // (P v)_t  (rows >= n are zero)
             double* vb = bcast(v);
             const int tt = opaque_t();
             double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+            if constexpr (LEAN) {
+                // a ROLLED loop over blocks of 8 (the row of K^-1 stays live across this: fully unrolled, the
+                // scheduler issues all 80 reads at once and the ADMM loop around it spills); same sums, same order
+                static_assert(NN % 8 == 0, "Pmul blocks");
+                const int rt = prow_base(tt);
+#pragma nounroll
+                for (int c0 = 0; c0 < NN; c0 += 8) {
 #pragma unroll
-            for (int j = 0; j < NN; ++j) sa[j & 7] = fma(s_P[paddr(j, tt)], vb[j], sa[j & 7]);
+                    for (int jj = 0; jj < 8; ++jj) sa[jj] = fma(prow_entry(c0 + jj, tt, rt), vb[c0 + jj], sa[jj]);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NN; ++j) sa[j & 7] = fma(s_P[paddr(j, tt)], vb[j], sa[j & 7]);
+            }
             return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
         };
         double Krow[NN];
@@ -694,25 +802,47 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             // (one wave issues an f64 op about every 8 cycles, so 4 chains keep it busy; 8 cost 4 more adds)
             double sa[4] = {0.0, 0.0, 0.0, 0.0};
             const double* vbuf = (slot >= 0) ? bcast_at(v, slot) : bcast(v);
-            if constexpr (NN <= 64) {
+            if constexpr (NN <= 64 && !CMP) {
                 double vb[NN];
                 lds_load_all<NN>(vbuf, vb);
 #pragma unroll
                 for (int j = 0; j < NN; ++j) sa[j & 3] = fma(Krow[j], vb[j], sa[j & 3]);
             } else {
                 // NN = 80: the whole vector in flight (160 VGPRs beside the 160 of Krow) spills inside the
-                // ADMM loop; 16 values at a time, same FMA order
-                constexpr int CH = 16;
-                static_assert(NN % CH == 0, "chunked broadcast");
+                // ADMM loop; CMP: the 3-wave budget (168) holds the row and a chunk.  CH values at a time
+                // (the next chunk's reads issued before this chunk's FMAs), same FMA order
+                constexpr int CH = CMP ? TGMPC_KCH : 16;
+                static_assert(NN % CH == 0 && CH % 2 == 0, "chunked broadcast");
+                const double2* v2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vbuf, 16));
+                double2 vb[CH / 2];
+#pragma unroll
+                for (int i = 0; i < CH / 2; ++i) vb[i] = v2[i];
 #pragma unroll
                 for (int c0 = 0; c0 < NN; c0 += CH) {
-                    double vb[CH];
-                    lds_load_all<CH>(vbuf + c0, vb);
+                    double2 vn[CH / 2];
 #pragma unroll
-                    for (int j = 0; j < CH; ++j) sa[(c0 + j) & 3] = fma(Krow[c0 + j], vb[j], sa[(c0 + j) & 3]);
+                    for (int i = 0; i < CH / 2; ++i) if (c0 + CH < NN) vn[i] = v2[(c0 + CH) / 2 + i];
+#pragma unroll
+                    for (int i = 0; i < CH / 2; ++i) {
+                        sa[(c0 + 2 * i) & 3] = fma(Krow[c0 + 2 * i], vb[i].x, sa[(c0 + 2 * i) & 3]);
+                        sa[(c0 + 2 * i + 1) & 3] = fma(Krow[c0 + 2 * i + 1], vb[i].y, sa[(c0 + 2 * i + 1) & 3]);
+                    }
+#pragma unroll
+                    for (int i = 0; i < CH / 2; ++i) vb[i] = vn[i];
+                }
+                // the reads one chunk ahead of the FMAs that use them (a read group per chunk, then the FMAs of
+                // the previous chunk); without this the scheduler issues every read first
+                __builtin_amdgcn_sched_group_barrier(0x100, CH / 2, 0);
+#pragma unroll
+                for (int c0 = 0; c0 < NN; c0 += CH) {
+                    if (c0 + CH < NN) __builtin_amdgcn_sched_group_barrier(0x100, CH / 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, CH, 0);
                 }
             }
-            return own ? (sa[0] + sa[1]) + (sa[2] + sa[3]) : 0.0;
+            double r = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+            // (opaque: keeps the compiler from turning the select into a branch around the whole mat-vec)
+            asm volatile("" : "+v"(r));
+            return own ? r : 0.0;
         };
         auto rho_for = [&](double l, double u, double rho) -> double {
             if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
@@ -724,9 +854,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         //   pr, max(|Ax|, |z|), dr, max(|Px|, |A'y|, |q|) (unscaled); prs, drs, pn, dn (scaled)
         struct Res { double pr, dr, eps_p, eps_d, prs, drs, pn, dn; };
         auto residuals = [&](double x, double zb, double zr, double yb, double yr) -> Res {
+            double px = Pmul(x);   // (first: its temporaries then coexist with no other)
             double axb, axr;
             Ax(x, axb, axr);
-            double px = Pmul(x);
             double aty = ATw(yb, yr);
             double v[8];
             if (own) {
@@ -748,7 +878,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 // of value i over lanes [p NN/8, (p+1) NN/8), three DPP steps join the 8 parts, and the 8
                 // maxima come back as one broadcast read -- ~30 instructions where 8 butterflies take ~180.
                 // NaN anywhere in a value makes that maximum NaN (as wave_max_dpp).
-                static_assert(NN % 8 == 0 && 8 * NN <= 2 * 4 * 16 * ((NN + 15) / 16), "s_F too small");
+                static_assert(NN % 8 == 0 && 8 * NN <= (CMP ? NU : NFS), "s_F too small");
                 constexpr int PL = NN / 8;
                 bool nan[8];
 #pragma unroll
@@ -776,12 +906,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             } else {
                 block_max(v);
             }
+            // (the results are uniform: held in SGPRs, uniformize, not in VGPRs across the solve)
             Res r;
-            r.pr = v[0];
-            r.eps_p = c.eps_abs + c.eps_rel * v[1];
-            r.dr = v[2];
-            r.eps_d = c.eps_abs + c.eps_rel * v[3];
-            r.prs = v[4]; r.drs = v[5]; r.pn = v[6]; r.dn = v[7];
+            r.pr = uniformize(v[0]);
+            r.eps_p = uniformize(c.eps_abs + c.eps_rel * v[1]);
+            r.dr = uniformize(v[2]);
+            r.eps_d = uniformize(c.eps_abs + c.eps_rel * v[3]);
+            r.prs = uniformize(v[4]); r.drs = uniformize(v[5]); r.pn = uniformize(v[6]); r.dn = uniformize(v[7]);
             return r;
         };
 
@@ -806,7 +937,29 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 if (w1 != 0.0) rho = fmin(fmax(w0, RHO_MIN), RHO_MAX);
             }
         }
-        double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
+        double rb, rr;   // rho of the box and rate rows (their inverses: pair row P_RHOI)
+        auto rho_rows = [&]() {
+            const dpair bb = pair(P_BB), br = pair(P_BR);
+            rb = rho_for(bb.x, bb.y, rho);
+            rr = rho_for(br.x, br.y, rho);
+            set_pair(P_RHOI, 1.0 / rb, 1.0 / rr);
+        };
+        rho_rows();
+        // LEAN: the per-lane constants of the ADMM loop re-formed from LDS at the K build and after the sweep (the
+        // same products of the same values, bit for bit), so that none of them is live across the factorization
+        auto reload = [&]() {
+            if constexpr (LEAN) {
+                const double Dl = cold(C_D), Ebl = cold(C_EB), Erl = cold(C_ER);
+                a_b = Ebl * Dl;
+                a_r = Erl * Dl;
+                const double Ddn = exch(Dl, -2);
+                a_rm = (t >= 2) ? Erl * Ddn : 0.0;
+                qi = cold(C_Q);
+                const dpair bb = pair(P_BB), br = pair(P_BR);
+                rb = rho_for(bb.x, bb.y, rho);
+                rr = rho_for(br.x, br.y, rho);
+            }
+        };
         Res r = {0, 0, 0, 0, 0, 0, 0, 0};
         int rounds = 0, ps = 0, actb = 0, actr = 0;
         double escale = 1.0;
@@ -814,20 +967,38 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         iter = 1;
         int nfact = 0;
         // diagnostics (traj_debug_set_stamps): cycles in residual checks / sweeps / polish
-        const bool prof = a.dbg != nullptr;
+        const bool prof = dbg != nullptr;
         long long cyc_res = 0, cyc_sweep = 0, cyc_pol = 0, n_res = 0, t_mark = 0;
         bool pol_open = false;
         auto tic = [&]() { if (prof) t_mark = __builtin_amdgcn_s_memtime(); };
         auto toc = [&](long long& acc) { if (prof) acc += __builtin_amdgcn_s_memtime() - t_mark; };
+        // LEAN: the iterate is parked in LDS (past the sweep's pivot columns) from before the K build to after the
+        // sweep -- the factorization is the kernel's register peak, and values live across it are spilled
+        typedef __attribute__((address_space(3))) volatile double* LdsVDs;
+        auto stash = [&]() {
+            if constexpr (LEAN) {
+                LdsVDs sp = (LdsVDs)(s_u + ((NSW + 1) & ~1));
+                if (t < NN) { sp[t] = x; sp[NN + t] = zb; sp[2 * NN + t] = zr; sp[3 * NN + t] = yb; sp[4 * NN + t] = yr; }
+            }
+        };
+        auto unstash = [&]() {
+            if constexpr (LEAN) {
+                LdsVDs sp = (LdsVDs)(s_u + ((NSW + 1) & ~1));
+                x = sp[tc]; zb = sp[NN + tc]; zr = sp[2 * NN + tc]; yb = sp[3 * NN + tc]; yr = sp[4 * NN + tc];
+            }
+        };
         while (phase != PH_DONE) {
             if (pol_open) { toc(cyc_pol); pol_open = false; }
             ++nfact;
+            stash();
+            reload();
             // ---- build K (row t) ----
             const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
             const double kr = (phase == PH_ADMM) ? rr : (actr ? 1.0 / dl : 0.0);
             const double ks = (phase == PH_ADMM) ? sig : dl;
             {
                 const double kr_up = exch(kr, +2);
+                const double a_rp = exch(a_rm, +2);   // = Er(t+2) D(t), bit for bit
                 const double dii = ks + kb * a_b * a_b + kr * a_r * a_r + kr_up * a_rp * a_rp;
                 // (t, t+2); by symmetry also the (t+2, t) entry: lane t+2's -kr a_r a_rm is the same product
                 // of the same values (kr_up = kr(t+2), cold(C_ARUP) = a_r(t+2), a_rp = Er(t+2) D(t) = a_rm(t+2))
@@ -906,10 +1077,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const int o = pv & 1;
                     const double* prow = s_sw + o * SB + o + pv;
                     const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
-                    double2 pr[NN / 2];
+                    // CMP: the pivot row in chunks of PC double2, the next chunk's reads issued before this
+                    // chunk's FMAs (the whole row beside Krow does not fit the 3-wave budget)
+                    constexpr int PC = CMP ? TGMPC_PCH : NN / 2 - 1;
+                    const double2 p0 = prow2[0];
+                    double2 pr[PC];
 #pragma unroll
-                    for (int i = 0; i < NN / 2; ++i) pr[i] = prow2[i];
-                    const double d = pr[0].x;
+                    for (int i = 0; i < PC; ++i) if (1 + i < NN / 2) pr[i] = prow2[1 + i];
+                    const double d = p0.x;
                     ok = ok && (d > 0.0);
                     const double dinv = rcp_nr(d);
                     const int rl = pv < SPARE ? NN + pv : pv - SPARE;   // receiver lane (uniform)
@@ -918,14 +1093,29 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const double be = recv ? dinv : -fd;
                     const double k0 = recv ? -dinv : fd;
                     rho = recv ? pv : ((t == pv) ? -1 : rho);
-                    const double n0 = fma3(be, pr[0].y, Krow[1]);
+                    const double n0 = fma3(be, p0.y, Krow[1]);
                     if (rho >= 0) {
                         double* nb = s_sw + (o ^ 1) * SB + (o ^ 1);
                         nb[rho] = n0;
                         nb[rho + NN] = n0;
                     }
+                    // Krow[j - 1] <- be * (pivot row)[j] + Krow[j], j = 2 .. NN-1: double2 i = 1 .. NN/2 - 1
 #pragma unroll
-                    for (int j = 2; j < NN; ++j) Krow[j - 1] = fma3(be, (j & 1) ? pr[j >> 1].y : pr[j >> 1].x, Krow[j]);
+                    for (int c = 1; c < NN / 2; c += PC) {
+                        double2 pn[PC];
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) if (c + PC + i < NN / 2) pn[i] = prow2[c + PC + i];
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) {
+                            if (c + i < NN / 2) {
+                                const int j = 2 * (c + i);
+                                Krow[j - 1] = fma3(be, pr[i].x, Krow[j]);
+                                Krow[j] = fma3(be, pr[i].y, Krow[j + 1]);
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) pr[i] = pn[i];
+                    }
                     Krow[0] = n0;
                     Krow[NN - 1] = k0;
                 }
@@ -995,6 +1185,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #if TGMPC_PRIO_SWEEP
             if (FUSED) __builtin_amdgcn_s_setprio(0);
 #endif
+            unstash();
+            reload();
             if (!ok) {
                 if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
                 // failed reduced-KKT factorization = unsuccessful polish (polish.c): the ADMM
@@ -1012,24 +1204,25 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 
             if (phase == PH_ADMM) {
                 bool converged = false, refactor = false;
-                const double rb_inv = 1.0 / rb, rr_inv = 1.0 / rr;
                 int chk = c.check_interval - (iter - 1) % c.check_interval;
-                const double oma = 1.0 - alpha;
+                const double oma = uniformize(1.0 - alpha);
                 for (; iter <= c.max_iter; ++iter) {
                     // OSQP's update_xz_tilde / update_x / update_z / update_y, each product-sum as an fma
                     // (the iteration is f64-issue bound: 69 f64 ops instead of 86; the oracle keeps OSQP's
                     // separate multiplies -- ulp-level differences, like its Cholesky vs this inverse)
                     // rhs = sig x - q + A'(rho z - y)
                     const double wb = fma(rb, zb, -yb), wr = fma(rr, zr, -yr);
-                    const double wr_up = (WAVES > 1) ? exch_at(wr, +2, 4) : exch(wr, +2);
-                    const double atw = fma(a_b, wb, fma(a_r, wr, -(a_rp * wr_up)));
+                    // a_rp(t) wr(t+2) formed on lane t+2 (a_rm(t+2) = a_rp(t) bit for bit)
+                    const double rp_up = (WAVES > 1) ? exch_at(a_rm * wr, +2, 4) : exch(a_rm * wr, +2);
+                    const double atw = fma(a_b, wb, fma(a_r, wr, -rp_up));
                     double xt = Kmul(fma(sig, x, atw - qi), WAVES > 1 ? 5 : -1);
                     const double xt_dn = (WAVES > 1) ? exch_at(xt, -2, 6) : exch(xt, -2);
                     const double ztb = a_b * xt, ztr = fma(a_r, xt, -(a_rm * xt_dn));
                     double xn = fma(alpha, xt, oma * x);
                     double zrb = fma(alpha, ztb, oma * zb);
                     double zrr = fma(alpha, ztr, oma * zr);
-                    double nzb = clampd(fma(rb_inv, yb, zrb), slb, sub), nzr = clampd(fma(rr_inv, yr, zrr), slr, sur);
+                    const dpair ri = pair(P_RHOI), bb = pair(P_BB), br = pair(P_BR);   // (LDS, see the cold values)
+                    double nzb = clampd(fma(ri.x, yb, zrb), bb.x, bb.y), nzr = clampd(fma(ri.y, yr, zrr), br.x, br.y);
                     yb = fma(rb, zrb - nzb, yb);
                     yr = fma(rr, zrr - nzr, yr);
                     x = xn;
@@ -1051,9 +1244,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                             double est = rho * sqrt((r.prs / (r.pn + DIV_TOL)) / (r.drs / (r.dn + DIV_TOL) + DIV_TOL));
                             est = fmin(fmax(est, RHO_MIN), RHO_MAX);
                             if (est > rho * c.adaptive_rho_tol || est < rho / c.adaptive_rho_tol) {
-                                rho = est;
-                                rb = rho_for(slb, sub, rho);
-                                rr = rho_for(slr, sur, rho);
+                                rho = uniformize(est);
+                                rho_rows();
                                 refactor = true;
                                 ++iter;
                                 break;
@@ -1073,6 +1265,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 }
                 if (status == TRAJ_STATUS_OPTIMAL && c.polish) {
                     // OSQP active sets: lower if z - l < -y, upper if u - z < y
+                    const dpair bb = pair(P_BB), br = pair(P_BR);
+                    const double slb = bb.x, sub = bb.y, slr = br.x, sur = br.y;
                     actb = own ? ((zb - slb < -yb) ? -1 : ((sub - zb < yb) ? 1 : 0)) : 0;
                     actr = own ? ((zr - slr < -yr) ? -1 : ((sur - zr < yr) ? 1 : 0)) : 0;
                     ps = 1;
@@ -1087,6 +1281,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             tic();
             pol_open = true;
             {
+                double slb, sub, slr, sur;   // scaled bounds (re-read from LDS where used)
+                auto bounds = [&]() {
+                    const dpair bb2 = pair(P_BB), br2 = pair(P_BR);
+                    slb = bb2.x; sub = bb2.y; slr = br2.x; sur = br2.y;
+                };
+                bounds();
                 const double bb = actb < 0 ? slb : (actb > 0 ? sub : 0.0);
                 const double br = actr < 0 ? slr : (actr > 0 ? sur : 0.0);
                 double px_ = 0.0, pyb = 0.0, pyr = 0.0;
@@ -1111,6 +1311,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 if (c.polish_mode == 0) {
                     // z = proj(Ax + y), y = Ax + y - z (OSQP project_normalcone); accept if residuals drop
                     double ztb = axb + pyb, ztr = axr + pyr;
+                    bounds();
                     double nzb = clampd(ztb, slb, sub), nzr = clampd(ztr, slr, sur);
                     double nyb = ztb - nzb, nyr = ztr - nzr;
                     Res rp = residuals(px_, nzb, nzr, nyb, nyr);
@@ -1129,7 +1330,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 const double tol = c.cert_tol;
                 double v[2];
                 const double Dinv = 1.0 / cold(C_D), Ebinv = 1.0 / cold(C_EB), Erinv = 1.0 / cold(C_ER);
-                const double lb = cold(C_LB), ub = cold(C_UB), lr = cold(C_LR), ur = cold(C_UR);
+                double lb, ub, lr, ur;
+                raw_bounds(lb, ub, lr, ur);
+                bounds();
                 v[0] = own ? fabs(Dinv * (Pxv + qi + atyv)) * csinv : 0.0;            // stationarity
                 v[1] = own ? fmax(fabs(Dinv * qi), fabs(Dinv * Pxv)) * csinv : 0.0;  // gradient scale
                 block_max(v);
@@ -1286,7 +1489,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     st_coh(m, (step == a.nsteps - 1) ? acc / a.nsteps : acc);
                 }
                 if (step == a.nsteps - 1) stamp(23, __builtin_amdgcn_s_memrealtime());   // launch span
-                if (a.dbg_items) a.dbg_items[4 * (size_t)item_of_wave + 2] = __builtin_amdgcn_s_memrealtime();
+                if (dbg_items) dbg_items[4 * (size_t)item_of_wave + 2] = __builtin_amdgcn_s_memrealtime();
                 // hand the instance to whichever workgroup takes its next step: the sc1 state stores
                 // complete (vmcnt(0)), then the step counter is stored sc1 (no L2 writeback)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

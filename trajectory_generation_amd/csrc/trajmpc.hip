@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <atomic>
 #include <cstring>
 #include <vector>
 
@@ -234,6 +235,14 @@ static int launch_general(const KArgs& a, double* gws, hipStream_t st) {
 static long long* g_dbg = nullptr;  // diagnostics buffer (traj_debug_set_stamps)
 static long long* g_dbg_items = nullptr;  // fused-run item timeline (traj_debug_set_item_stamps)
 static int g_fused_grid = 0;        // traj_debug_fused_grid
+// fused runs of at least this many steps use the 3-waves-per-SIMD kernel (capacity 40): more throughput once
+// the launch is bound by its bulk (bench workload, 200 steps: 14.35 M vs 13.51 M steps/s) but each item's latency
+// grows, and a shorter launch is bound by its heaviest instances' chains of items (20 steps: 10.1 M vs 11.7 M;
+// 100 steps: 10.4 M vs 12.1 M) -- DESIGN.md section 5
+#ifndef TRAJ_FUSED_W3_MIN_STEPS
+#define TRAJ_FUSED_W3_MIN_STEPS 200
+#endif
+static int g_fused_waves = 0;       // traj_debug_fused_waves: 0 = by launch length, 2 or 3 = forced
 static int g_spin_limit = 1 << 22;  // traj_debug_spin_limit: polls before a fused hand-off is declared lost
 static int g_lead_steps = TGMPC_LEAD_STEPS, g_lead_permille = TGMPC_LEAD_PERMILLE;   // traj_debug_queue_lead
 
@@ -268,6 +277,12 @@ int traj_debug_set_item_stamps(long long* buf) {
 int traj_debug_fused_grid(int workgroups) {
     if (workgroups < 0) return TRAJ_E_ARG;
     g_fused_grid = workgroups;
+    return TRAJ_OK;
+}
+
+int traj_debug_fused_waves(int waves) {
+    if (waves != 0 && waves != 2 && waves != 3) return TRAJ_E_ARG;
+    g_fused_waves = waves;
     return TRAJ_OK;
 }
 
@@ -575,6 +590,7 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.dbg = g_dbg;
     a.nsteps = steps;
     a.fused_grid = g_fused_grid;
+    a.wps = g_fused_waves ? g_fused_waves : (steps >= TRAJ_FUSED_W3_MIN_STEPS ? 3 : 2);
     a.spin_limit = g_spin_limit;
     a.dbg_items = g_dbg_items;
     carve_workspace(a, workspace, B, c->N);
@@ -589,10 +605,13 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
         // a run's first launch has no previous order, so order_kernel first runs on the SECOND launch; load
         // its code object now (HIP loads kernels lazily, ~0.75 ms of host time on the first launch) so that
         // cost is not paid inside a later, timed launch
-        static bool order_loaded = false;
-        if (!order_loaded) {
+        // (per device: HIP loads code objects per device; one process may drive several GPUs)
+        static std::atomic<bool> order_loaded[64];
+        int dev = 0;
+        if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && !order_loaded[dev].load()) {
             hipFuncAttributes fa;
-            order_loaded = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&order_kernel)) == hipSuccess;
+            if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&order_kernel)) == hipSuccess)
+                order_loaded[dev].store(true);
         }
     }
     if (t0 > 0) {
