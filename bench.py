@@ -197,10 +197,12 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
     return out
 
 
-def _spawn_workers(n):
+def _spawn_workers(n, poll_s=0.2, grace_s=10.0, cmd=None):
     """bench.py --gpus N without a launcher: N worker processes (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous
-    on 127.0.0.1), each runs this script on its own GPU over RCCL; the parent never touches the GPU and
-    exits with the first non-zero worker status."""
+    on 127.0.0.1), each runs this script on its own GPU over RCCL; the parent never touches the GPU.  It polls
+    every worker: on the first non-zero exit the others are terminated (then killed after grace_s) -- a rank
+    that dies before or inside the rendezvous must not leave its siblings blocked -- and the parent exits with
+    that status."""
     import socket
     import subprocess
     s = socket.socket()
@@ -211,39 +213,109 @@ def _spawn_workers(n):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    codes = [p.wait() for p in procs]
-    bad = [c for c in codes if c != 0]
-    if bad:
-        sys.exit(bad[0])
+        procs.append(subprocess.Popen(cmd or ([sys.executable, os.path.abspath(__file__)] + sys.argv[1:]), env=env))
+    failed = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c is not None and c != 0]
+        if bad:
+            failed = bad[0]
+            break
+        if all(c is not None for c in codes):
+            break
+        time.sleep(poll_s)
+    if failed:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.0, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        sys.exit(failed)
 
 
-def dataset_leg(args, w, dev, dist, rank, world):
+class GpuOps:
+    """The bench's device side on this rank's GPU: the closed loop through libtrajmpc.so (fused launches, or
+    one traj_closed_loop_step sequence per step), timed with HIP events on the launch stream."""
+
+    def __init__(self, local: int):
+        self.dev = TB.require_gpu(f"cuda:{local}")
+        torch.cuda.set_device(self.dev)
+
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def setup(self, w, B, N, Ts, T, polish_mode, warm_start=1):
+        paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=self.dev)
+        st = dict(paths=paths, cfg=TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode, warm_start=warm_start),
+                  x=torch.as_tensor(w["x0"], device=self.dev).contiguous(),
+                  u=torch.as_tensor(w["u0"], device=self.dev).contiguous(),
+                  vref=torch.as_tensor(np.tile(w["vref"], (B, 1)), device=self.dev).contiguous(),
+                  hx=torch.empty((B, T + 1, 6), dtype=torch.float64, device=self.dev),
+                  hu=torch.empty((B, T, 2), dtype=torch.float64, device=self.dev),
+                  st=torch.empty((T, B), dtype=torch.int32, device=self.dev),
+                  it=torch.empty((T, B), dtype=torch.int32, device=self.dev), kmax=int(paths.xk.shape[1]))
+        st["hx"][:, 0] = st["x"]
+        return st
+
+    def run(self, s, t0, steps, fused):
+        """Steps t0 .. t0+steps-1 (one fused launch, or the per-step launches)."""
+        if fused:
+            TB.closed_loop_run(s["x"], s["u"], s["paths"], s["vref"], s["cfg"], None, t0, steps, s["hx"], s["hu"],
+                               s["st"][t0:t0 + steps], s["it"][t0:t0 + steps])
+        else:
+            for k in range(steps):
+                t = t0 + k
+                TB.closed_loop_step(s["x"], s["u"], s["paths"], s["vref"], s["cfg"], None, t, s["hx"], s["hu"],
+                                    s["st"][t], s["it"][t])
+
+    def kernel_timing(self, steps):
+        _lib.check(_lib.lib().traj_debug_kernel_timing(steps), "traj_debug_kernel_timing")
+
+    def kernel_times(self):
+        L = _lib.lib()
+        kms = (ctypes.c_double * 4)()
+        nts = ctypes.c_int(0)
+        _lib.check(L.traj_debug_kernel_times(kms, ctypes.byref(nts)), "traj_debug_kernel_times")
+        _lib.check(L.traj_debug_kernel_timing(0), "traj_debug_kernel_timing")
+        return dict(zip(("rollout_kernel", "jac_kernel", "order_kernel", "solve_kernel"), list(kms)))
+
+    def closed_loop(self, w, T, N, Ts, polish_mode):
+        """The dataset leg's closed loop of this rank's trajectories: X [B,T+1,6], U [B,T,2], status [T,B]."""
+        paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=self.dev)
+        res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T,
+                                 TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode))
+        return res["X"], res["U"], res["status"]
+
+
+def dataset_leg(args, w, ops, dist, rank, world):
     """BASELINE.json configs[3] on this node: every rank runs the closed loop of its --batch trajectories
     (ids rank * B + i, the bench workload) for --dataset-steps steps from the initial states, the packed
     [B, T+1, 9] histories go to rank 0 with one dist.gather (RCCL over xGMI), and rank 0 optionally
     writes the CSVs.  Generation, gather and CSV writing are timed separately (max over ranks)."""
     from trajectory_generation_amd import dataset as D
     B, N, Ts, T = args.batch, args.horizon, args.dt, args.dataset_steps
-    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=dev)
-    cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=args.polish_mode)
 
     def bar():
-        torch.cuda.synchronize()
+        ops.sync()
         if dist:
             dist.barrier()
-        torch.cuda.synchronize()
+        ops.sync()
 
     bar()
     t0 = time.perf_counter()
-    res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg)
-    blk = D.pack_history(res["X"], res["U"], res["status"])
+    X, U, status = ops.closed_loop(w, T, N, Ts, args.polish_mode)
+    blk = D.pack_history(X, U, status)
     bar()
     t1 = time.perf_counter()
     full = D.gather_to_root(blk, dist)
     bar()
     t2 = time.perf_counter()
-    times = torch.tensor([t1 - t0, t2 - t1], dtype=torch.float64, device=dev)
+    times = torch.tensor([t1 - t0, t2 - t1], dtype=torch.float64, device=ops.dev)
     if dist:
         dist.all_reduce(times, op=dist.ReduceOp.MAX)
     gen_s, gather_s = (float(v) for v in times.cpu())
@@ -264,7 +336,7 @@ def dataset_leg(args, w, dev, dist, rank, world):
             "csv_s": csv_s, "status_hist": torch.bincount(st.reshape(-1).long(), minlength=7).tolist()}
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -291,8 +363,17 @@ def main():
                          "many steps, then the histories gathered into rank 0 (0 disables)")
     ap.add_argument("--dataset-csv", default=None,
                     help="directory: rank 0 also writes the dataset CSVs there (timed separately)")
-    args = ap.parse_args()
+    ap.add_argument("--no-cold", action="store_true",
+                    help="skip the reference-semantics (cold-start) pass reported as 'cold'")
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="seconds before a process-group rendezvous or collective gives up (N > 1)")
+    return ap.parse_args(argv)
 
+
+def main(argv=None, ops_factory=None, backend=None):
+    """The bench.  ops_factory(local_rank) gives the device side (default GpuOps); backend the process-group
+    backend (default nccl = RCCL; tests pass gloo with a CPU stand-in)."""
+    args = parse_args(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # no launcher: start one worker process per GPU before anything in this process touches the GPU
         return _spawn_workers(args.gpus)
@@ -303,83 +384,90 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     world = 1
+    backend = backend or os.environ.get("TRAJ_BENCH_BACKEND", "nccl")
     if world_env > 1:
+        import datetime
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        kw = {}
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=args.dist_timeout), **kw)
         world = dist.get_world_size()
         assert world == world_env
-    dev = TB.require_gpu(f"cuda:{local}")
-    torch.cuda.set_device(dev)
+    ops = (ops_factory or GpuOps)(local)
+    try:
+        out = bench_run(args, ops, dist, rank, world)
+    finally:
+        if dist:
+            dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    return out
 
+
+def bench_run(args, ops, dist, rank, world):
+    """One rank's bench: warmup, the timed region bracketed by barrier + synchronize on both sides, the
+    max-over-ranks elapsed time, the dataset leg; rank 0 returns the JSON record (None elsewhere)."""
     N, Ts, B = args.horizon, args.dt, args.batch
     w = make_workload(B, N, Ts, kind=args.kind, seed=0, id_offset=rank * B)
-    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=dev)
-    x = torch.as_tensor(w["x0"], device=dev).contiguous()
-    u = torch.as_tensor(w["u0"], device=dev).contiguous()
-    vref = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=dev).contiguous()
-    cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=args.polish_mode)
     T = args.warmup + args.steps
-    hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=dev)
-    hu = torch.empty((B, T, 2), dtype=torch.float64, device=dev)
-    hx[:, 0] = x
-    st = torch.empty((T, B), dtype=torch.int32, device=dev)
-    it = torch.empty((T, B), dtype=torch.int32, device=dev)
-
     fused = not args.per_step
-    if fused:
+
+    def timed_pass(warm_start, timing):
+        """W untimed warmup steps, then EXACTLY K timed steps bracketed by barrier + synchronize on both
+        sides; the elapsed time is the max over ranks."""
+        s = ops.setup(w, B, N, Ts, T, args.polish_mode, warm_start=warm_start)
         if args.warmup:
-            TB.closed_loop_run(x, u, paths, vref, cfg, None, 0, args.warmup, hx, hu, st[:args.warmup], it[:args.warmup])
-    else:
-        for t in range(args.warmup):
-            TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
+            ops.run(s, 0, args.warmup, fused)
+        ops.sync()
+        if dist:
+            dist.barrier()
+        ops.sync()
+        if timing:
+            ops.kernel_timing(args.steps)
+        t0 = time.perf_counter()
+        ops.run(s, args.warmup, args.steps, fused)   # fused: all K steps in one launch (= K step launches)
+        ops.sync()
+        if dist:
+            dist.barrier()
+        ops.sync()
+        elapsed = time.perf_counter() - t0
+        if dist:
+            e = torch.tensor([elapsed], dtype=torch.float64, device=ops.dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            elapsed = float(e.item())
+        return s, elapsed
 
-    L = _lib.lib()
-    _lib.check(L.traj_debug_kernel_timing(args.steps), "traj_debug_kernel_timing")
-    t0 = time.perf_counter()
-    if fused:   # all K steps in one launch (traj_closed_loop_run: bit-identical to K step launches)
-        w0 = args.warmup
-        TB.closed_loop_run(x, u, paths, vref, cfg, None, w0, args.steps, hx, hu, st[w0:], it[w0:])
-    else:
-        for k in range(args.steps):
-            t = args.warmup + k
-            TB.closed_loop_step(x, u, paths, vref, cfg, None, t, hx, hu, st[t], it[t])
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-
-    kms = (ctypes.c_double * 4)()
-    nts = ctypes.c_int(0)
-    _lib.check(L.traj_debug_kernel_times(kms, ctypes.byref(nts)), "traj_debug_kernel_times")
-    _lib.check(L.traj_debug_kernel_timing(0), "traj_debug_kernel_timing")
-    kernels_ms = dict(zip(("rollout_kernel", "jac_kernel", "order_kernel", "solve_kernel"), list(kms)))
+    # the headline: the closed loop's warm start (each step's ADMM from the rho the previous step adapted to;
+    # the polished optimum does not depend on rho).  The reference solves cold every step -- a new cp.Problem
+    # per call makes its warm_start=True a no-op (mpc_6stati.py:252-256) -- reported beside it ("cold").
+    s, elapsed = timed_pass(1, True)
+    kernels_ms = ops.kernel_times()
+    s_cold = cold = None
+    if not args.no_cold:
+        s_cold, el_cold = timed_pass(0, False)
+        ic = s_cold["it"][args.warmup:].cpu().numpy().reshape(-1)
+        cold = {"what": "the same command with warm_start=0 (cold rho every step, the reference's effective "
+                        "semantics, mpc_6stati.py:252-256)",
+                "value": world * B * args.steps / el_cold, "ms_per_step": 1e3 * el_cold / args.steps,
+                "iters_mean": float(ic.mean()), "iters_p99": float(np.percentile(ic, 99)), "iters_max": int(ic.max()),
+                "status_hist": np.bincount(s_cold["st"][args.warmup:].cpu().numpy().reshape(-1), minlength=7).tolist()}
     if fused:   # one launch = args.steps closed-loop steps, linearization inside the solve kernel
         kernels_ms = {"solve_kernel": kernels_ms["solve_kernel"]}
     kern_ms = kernels_ms["solve_kernel"]
     steps_per_launch = args.steps if fused else 1
-    iters = it[args.warmup:].cpu().numpy().reshape(-1)
-    stat = st[args.warmup:].cpu().numpy().reshape(-1)
-    dataset = dataset_leg(args, w, dev, dist, rank, world) if args.dataset_steps > 0 else None
+    iters = s["it"][args.warmup:].cpu().numpy().reshape(-1)
+    stat = s["st"][args.warmup:].cpu().numpy().reshape(-1)
+    dataset = dataset_leg(args, w, ops, dist, rank, world) if args.dataset_steps > 0 else None
     if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
+        return None
 
     total = world * B * args.steps
     value = total / elapsed
-    kmax = int(paths.xk.shape[1])
+    kmax = s["kmax"]
     bytes_launch = B * algorithmic_bytes_per_traj(N, kmax) * steps_per_launch
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
     traffic = traffic_step = None
     if os.path.exists(args.traffic_json):
         try:
@@ -443,9 +531,10 @@ def main():
         "config": {"workload": f"closed-loop {args.kind}-tracking MPC, {B} trajectories/GPU, N={N}, dt={Ts}s",
                    "global_batch": world * B, "horizon": N, "dt": Ts, "parallelism": f"shard{world}",
                    "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64",
+                   "warm_start": "rho carried from the instance's previous step (closed loop); cold: see 'cold'",
                    "launch": "fused traj_closed_loop_run" if fused else "traj_closed_loop_step per step"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
                      "kernel": f"solve_kernel<{_capacity(2 * N)},true>" + (
                          f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
                      "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
@@ -456,17 +545,18 @@ def main():
                          "iters_max": int(iters.max()),
                          "status_hist": np.bincount(stat, minlength=7).tolist()},
     }
+    out["cold"] = cold
     out["dataset"] = dataset
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(w, N, Ts, min(args.cpu_traj, B), args.cpu_steps, args.polish_mode,
-                                           cfg.warm_start)
+                                           s["cfg"].warm_start)
     else:
         out["cpu_baseline"] = None
     if not args.no_knet and world == 1:
-        out["knet"] = knet_measure(dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json)
-    print(json.dumps(out), flush=True)
-    if dist:
-        dist.destroy_process_group()
+        out["knet"] = knet_measure(ops.dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json)
+    return out
+
+
 
 
 if __name__ == "__main__":

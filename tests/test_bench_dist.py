@@ -1,0 +1,110 @@
+"""bench.py's multi-rank path on CPU (no GPU): bench_run's distributed branch end to end at world size 2
+over gloo -- barriers, the MAX all-reduce of the elapsed time, the dataset leg's gather into rank 0, the
+record on rank 0 only -- with a CPU stand-in for the device side; and the launcher's failure handling (a
+worker that dies takes its siblings down, the parent exits with its status)."""
+import os
+import socket
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+
+
+class CpuOps:
+    """Same interface as bench.GpuOps; deterministic arithmetic instead of the MPC (the test checks the
+    orchestration, not the solver)."""
+
+    def __init__(self, local):
+        self.dev = torch.device("cpu")
+
+    def sync(self):
+        pass
+
+    def setup(self, w, B, N, Ts, T, polish_mode, warm_start=1):
+        x = torch.as_tensor(w["x0"]).clone()
+        s = dict(x=x, hx=torch.zeros((B, T + 1, 6), dtype=torch.float64), hu=torch.zeros((B, T, 2), dtype=torch.float64),
+                 st=torch.zeros((T, B), dtype=torch.int32), it=torch.zeros((T, B), dtype=torch.int32), kmax=11,
+                 cfg=type("Cfg", (), {"warm_start": warm_start})())
+        s["hx"][:, 0] = x
+        return s
+
+    def run(self, s, t0, steps, fused):
+        for t in range(t0, t0 + steps):
+            s["x"] += 0.01
+            s["hx"][:, t + 1] = s["x"]
+            s["st"][t] = 0
+            s["it"][t] = 25 if s["cfg"].warm_start else 50
+        time.sleep(0.06 if os.environ.get("RANK") == "1" else 0.01)   # rank 1 is the slow one
+
+    def kernel_timing(self, steps):
+        pass
+
+    def kernel_times(self):
+        return {"rollout_kernel": 0.0, "jac_kernel": 0.0, "order_kernel": 0.0, "solve_kernel": 1.0}
+
+    def closed_loop(self, w, T, N, Ts, polish_mode):
+        x0 = torch.as_tensor(w["x0"])
+        B = x0.shape[0]
+        X = x0[:, None, :] + 0.01 * torch.arange(T + 1, dtype=torch.float64)[None, :, None]
+        U = torch.zeros((B, T, 2), dtype=torch.float64)
+        return X, U, torch.zeros((T, B), dtype=torch.int32)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank(rank, port, q):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import bench
+    out = bench.main(["--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "4", "--dataset-steps", "5",
+                      "--no-cpu", "--no-knet", "--dist-timeout", "120"], ops_factory=CpuOps, backend="gloo")
+    q.put((rank, out))
+
+
+def test_bench_run_two_ranks_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[1] is None                                   # one record, from rank 0
+    out = got[0]
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 8 and out["scaling"] == "weak"
+    assert out["value"] == pytest.approx(8 * 3 / (out["ms_per_step"] * 3 / 1e3))   # whole-job steps / max elapsed
+    assert out["ms_per_step"] >= 18.0                       # the MAX over ranks: rank 1's 60 ms for 3 steps
+    assert out["cold"]["iters_mean"] == 50.0 and out["solver_stats"]["iters_mean"] == 25.0
+    ds = out["dataset"]
+    assert ds["trajectories"] == 8 and ds["steps"] == 5 and ds["gather_bytes"] == 8 * 6 * 9 * 8
+    assert ds["status_hist"][0] == 8 * 5
+
+
+def test_spawned_worker_failure_stops_the_siblings():
+    """_spawn_workers: worker 1 exits 3 at once, worker 0 would sleep a minute -- the parent terminates it and
+    exits 3 within seconds (a rank that dies before the rendezvous must not leave the others blocked)."""
+    import bench
+    script = ("import os, sys, time\n"
+              "if os.environ['RANK'] == '1': sys.exit(3)\n"
+              "time.sleep(60)\n")
+    t0 = time.time()
+    with pytest.raises(SystemExit) as e:
+        bench._spawn_workers(2, poll_s=0.05, grace_s=5.0, cmd=[sys.executable, "-c", script])
+    assert e.value.code == 3
+    assert time.time() - t0 < 20

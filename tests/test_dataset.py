@@ -158,3 +158,22 @@ def test_native_loader_matches_pandas_loader(tmp_path):
             assert torch.equal(ta.nan_to_num(), tb.nan_to_num())
     assert D.load_vehicle_dataset(f"{p}_noisy.csv", f"{p}_clean.csv", T_steps=40, native=True) is None
     assert D.load_vehicle_dataset(str(tmp_path / "missing.csv"), f"{p}_clean.csv", native=True) is None
+
+
+def test_native_csv_reader_degenerate_files(tmp_path):
+    """traj_dataset_read_csv on an empty file and on a header with or without its newline: zero data rows
+    parse as OK, asking for rows that are not there is TRAJ_E_ARG (never a read past the buffer)."""
+    import ctypes as C
+    from trajectory_generation_amd import _lib
+    L = _lib.lib()
+    cases = {"empty": b"", "header_no_newline": b"X,Y,phi", "header_only": b"X,Y,phi\n"}
+    out = (C.c_double * 3)()
+    for name, data in cases.items():
+        p = tmp_path / f"{name}.csv"
+        p.write_bytes(data)
+        nc = C.c_int(0)
+        assert L.traj_dataset_csv_rows(str(p).encode(), C.byref(nc)) == 0, name
+        assert L.traj_dataset_read_csv(str(p).encode(), 0, 3, None, 2) == _lib.TRAJ_OK, name
+        assert L.traj_dataset_read_csv(str(p).encode(), 1, 3, out, 2) == _lib.TRAJ_E_ARG, name
+    names, buf = D.read_csv_native(str(tmp_path / "header_only.csv"))
+    assert names == ["X", "Y", "phi"] and tuple(buf.shape) == (0, 3)

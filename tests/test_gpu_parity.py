@@ -577,6 +577,34 @@ def test_state_bounds_edge_cases(gpu, oracle_lib):
     assert st in ("optimal", "optimal_inaccurate") and info["X_opt"].shape == (6, 21)
 
 
+def test_state_bound_solves_between_closed_loop_steps(gpu):
+    """A state-bound step / QP solve (whose scratch is the caller's workspace) made between two closed-loop
+    steps on the same stream leaves the closed loop's state (warm-start records, order, queue) alone: the
+    interleaved trajectory equals the uninterrupted one bit for bit (batch.workspace keeps one buffer per
+    role)."""
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B = 20, 0.05, 8, 24
+    w = make_workload(B, N, Ts, kind="spline", seed=4)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts)                     # warm start on: state carried between steps
+    ref = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    x = torch.as_tensor(w["x0"], device=gpu).clone()
+    u = torch.as_tensor(w["u0"], device=gpu).clone()
+    vr = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=gpu)
+    hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=gpu)
+    hu = torch.empty((B, T, 2), dtype=torch.float64, device=gpu)
+    hx[:, 0] = x
+    st = torch.empty((T, B), dtype=torch.int32, device=gpu)
+    it = torch.empty((T, B), dtype=torch.int32, device=gpu)
+    sb_cfg = TB.config_struct(N=N, Ts=Ts, x_lo=SB_LO, x_hi=SB_HI)
+    x0s, ups, prs, vrs = random_instances(31, 200, N, Ts)      # more instances than the closed loop: a bigger scratch
+    for t in range(T):
+        TB.closed_loop_step(x, u, paths, vr, cfg, None, t, hx, hu, st[t], it[t])
+        TB.mpc_step_batch(x0s, ups, prs, vrs, sb_cfg)          # state-bound step between the closed-loop steps
+    for k, v in (("X", hx), ("U", hu), ("status", st), ("iters", it)):
+        assert torch.equal(ref[k], v), k
+
+
 # ------------------------------------------------------------------ dataset emitter (f1)
 
 def test_dataset_generate_single_rank(gpu, oracle_lib, tmp_path):
@@ -594,6 +622,10 @@ def test_dataset_generate_single_rank(gpu, oracle_lib, tmp_path):
     assert np.array_equal(st.cpu().numpy(), r["status"].T)
     assert np.abs(X.cpu().numpy() - r["X"]).max() <= 1e-3
     assert st.shape == (T, B)
+    # pack_history -> gather_to_root -> unpack_history is an exact copy of the device closed loop
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    direct = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts))
+    assert torch.equal(X, direct["X"]) and torch.equal(U, direct["U"]) and torch.equal(st, direct["status"])
     clean = pd.read_csv(tmp_path / "ds_clean.csv", float_precision="round_trip")
     noisy = pd.read_csv(tmp_path / "ds_noisy.csv", float_precision="round_trip")
     assert len(clean) == B * (T + 1) and list(noisy.columns)[-1] == "trajectory_id"

@@ -93,7 +93,7 @@ def test_graph_runner_matches_eager_and_oracle(gpu):
     p.update(LIMITS)
     ref = KO.run_sequences(knet_weights(0), p, float(G["Ts"]), y.cpu().numpy(), u.cpu().numpy(), m1x0.cpu().numpy(),
                            G["x_mean"], G["x_std"], G["y_mean"], G["y_std"]).numpy()
-    assert np.abs(eager - ref).max() <= 1e-3 * (1 + np.abs(ref).max())
+    assert np.abs(eager - ref).max() <= 2e-4 * (1 + np.abs(ref).max())
 
 
 @pytest.mark.parametrize("B,T,groups,in_mult", [(64, 30, 1, 5), (7, 5, 1, 5), (1, 3, 1, 5), (37, 6, 3, 5),

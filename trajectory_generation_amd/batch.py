@@ -158,14 +158,22 @@ def _state_bounds(cfg: MpcConfig) -> bool:
     return any((cfg.has_x_lo and cfg.x_lo[i] > -1e30) or (cfg.has_x_hi and cfg.x_hi[i] < 1e30) for i in range(6))
 
 
-def workspace(B: int, N: int, device, extra_bytes: int = 0) -> torch.Tensor:
+def workspace(B: int, N: int, device, extra_bytes: int = 0, role: str = "closed_loop") -> torch.Tensor:
     """Cached device workspace for B instances of horizon N (traj_mpc_workspace_bytes), plus extra_bytes
-    (traj_mpc_sb_workspace_bytes: the state-bound solver's scratch, caller-owned like the rest)."""
+    (traj_mpc_sb_workspace_bytes: the state-bound solver's scratch, caller-owned like the rest).
+
+    One buffer per (device, stream, role).  The closed loop keeps state in its workspace between calls (the
+    warm-start records, the previous launch's order, the step queue), so the one-shot step / QP entry points
+    use a buffer of their own ("step"): a state-bound solve between two closed-loop steps on the same stream
+    must not overwrite -- or, by growing the cache, replace -- the closed loop's buffer."""
     nbytes = int(_lib.lib().traj_mpc_workspace_bytes(int(B), int(N))) + int(extra_bytes)
-    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream, role)
     ws = _WS.get(key)
     if ws is None or ws.numel() * 8 < nbytes:
-        ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+        new = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+        if ws is not None:
+            new[:ws.numel()].copy_(ws)   # (stream-ordered) what the smaller buffer held stays in place
+        ws = new
         _WS[key] = ws
     return ws
 
@@ -185,7 +193,7 @@ def mpc_step_batch(x0, u_prev, path_ref, vref, cfg: MpcConfig, params=None, out:
     vref = _dev(vref, (B, N + 1), dev)
     o = out if out is not None else _outputs(B, N, dev)
     sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _state_bounds(cfg) else 0
-    ws = workspace(B, N, dev, sb)
+    ws = workspace(B, N, dev, sb, role="step")
     _lib.check(_lib.lib().traj_mpc_step_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), _p(u_prev), _p(path_ref), _p(vref),
         _p(o["u_cmd"]), _p(o["status"]), _p(o["objective"]), _p(o["X_opt"]), _p(o["U_opt"]), _p(o["iters"]),
@@ -203,7 +211,7 @@ def mpc_qp_batch(x0, u_prev, path_ref, vref, Ad, Bd, g, cfg: MpcConfig, params=N
             _dev(Ad, (B, N, 6, 6), dev), _dev(Bd, (B, N, 6, 2), dev), _dev(g, (B, N, 6), dev)]
     o = _outputs(B, N, dev)
     sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _state_bounds(cfg) else 0
-    ws = workspace(0, N, dev, sb) if sb else None
+    ws = workspace(0, N, dev, sb, role="step") if sb else None
     _lib.check(_lib.lib().traj_mpc_qp_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), *[_p(a) for a in args],
         _p(o["u_cmd"]), _p(o["status"]), _p(o["objective"]), _p(o["X_opt"]), _p(o["U_opt"]), _p(o["iters"]),

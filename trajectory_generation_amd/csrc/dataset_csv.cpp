@@ -13,6 +13,7 @@
 // such a file, parsed in parallel chunks with std::from_chars into a caller buffer (row-major [rows, C],
 // float64; empty field = NaN), e.g. pinned host memory that is then copied to the device.
 #include <algorithm>
+#include <atomic>
 #include <charconv>
 #include <functional>
 #include <memory>
@@ -180,6 +181,10 @@ int traj_dataset_read_csv(const char* path, long long rows, int ncols, double* o
     std::fseek(f, 0, SEEK_END);
     const long size = std::ftell(f);
     std::fseek(f, 0, SEEK_SET);
+    if (size < 0) {
+        std::fclose(f);
+        return TRAJ_E_ARG;
+    }
     std::unique_ptr<char[]> data(new char[(size_t)size + 1]);   // no zero fill
     const bool rd = std::fread(data.get(), 1, (size_t)size, f) == (size_t)size;
     std::fclose(f);
@@ -188,6 +193,8 @@ int traj_dataset_read_csv(const char* path, long long rows, int ncols, double* o
     const char* base = data.get();
     const char* hdr_end = (const char*)std::memchr(base, '\n', (size_t)size + 1);
     const size_t p = (size_t)(hdr_end - base) + 1;
+    // an empty file, or a header with no newline (the sentinel's): no data lines at all
+    if (p > (size_t)size) return rows == 0 ? TRAJ_OK : TRAJ_E_ARG;
     // line starts after the header, found in parallel chunks (memchr) and concatenated in order
     const int nt = std::max(1, std::min(nthreads > 0 ? nthreads : 1, 64));
     std::vector<std::vector<size_t>> part(nt);
@@ -210,7 +217,7 @@ int traj_dataset_read_csv(const char* path, long long rows, int ncols, double* o
     starts.reserve((size_t)rows + 1);
     for (auto& v : part) starts.insert(starts.end(), v.begin(), v.end());
     if ((long long)starts.size() != rows) return TRAJ_E_ARG;
-    int err = 0;
+    std::atomic<int> err{0};   // set by any parsing thread
     run_threads((int)rows, nthreads > 0 ? nthreads : 1, [&](int, int r0, int r1) {
         for (int r = r0; r < r1; ++r) {
             const char* s = base + starts[r];
@@ -228,17 +235,17 @@ int traj_dataset_read_csv(const char* path, long long rows, int ncols, double* o
                         if (tok == "nan" || tok == "NaN") o[c] = NAN;
                         else if (tok == "inf") o[c] = INFINITY;
                         else if (tok == "-inf") o[c] = -INFINITY;
-                        else err = 1;
+                        else err.store(1, std::memory_order_relaxed);
                     }
                 }
                 if (c + 1 < ncols) {
-                    if (*e != ',') { err = 1; break; }
+                    if (*e != ',') { err.store(1, std::memory_order_relaxed); break; }
                     s = e + 1;
                 }
             }
         }
     });
-    return err ? TRAJ_E_ARG : TRAJ_OK;
+    return err.load() ? TRAJ_E_ARG : TRAJ_OK;
 }
 
 }  // extern "C"

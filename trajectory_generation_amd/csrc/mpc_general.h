@@ -16,8 +16,9 @@
 //     oracle's chol_solve adds them (ascending k forward, descending k backward);
 //   * -ffp-contract=off on both sides; division and sqrt are IEEE-rounded.
 // Layout: one 256-thread workgroup per instance; the Cholesky factor lives in LDS (n <= 80:
-// 51 KB); everything else in a per-call device scratch (traj_mpc_step_batch / traj_mpc_qp_batch
-// allocate it stream-ordered).  This path is for the optional argument only -- correctness first;
+// 51 KB); everything else in the caller's workspace: traj_mpc_sb_workspace_bytes(B, N) bytes past the step's
+// workspace (traj_mpc_step_batch) or the workspace argument of traj_mpc_qp_batch (ABI 2; the library never
+// allocates).  This path is for the optional argument only -- correctness first;
 // the 4096-trajectory closed loop never takes it.
 #pragma once
 #include "mpc_common.h"

@@ -138,8 +138,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // fused: the grid is the resident workgroups; each takes work items (step, rank) from a queue in
     // order -- all ranks of step 0, then of step 1, ... (rank = the previous launch's cost order) --
     // and waits, if it must, until the instance's previous step is complete.  The instance state
-    // (x, u_prev, warm-start record) passes between workgroups through global memory with agent-scope
-    // release / acquire on the per-instance step counter, so a slow solve delays only its instance
+    // (x, u_prev, warm-start record) passes between workgroups through global memory -- coherent (sc1) stores
+    // drained with vmcnt(0), then the per-instance step counter stored sc1; the consumer polls the counter and
+    // reads the state with sc1 loads (st_coh / ld_coh above, the hand-off at the end of the item) -- so a slow
+    // solve delays only its instance
     // and every slot stays busy until the queue is drained.
     bool more = true;
     int item_of_wave = 0;   // fused: the current work item (diagnostics)

@@ -4,7 +4,12 @@ The reference's only closed-loop caller is MPC/main.py:85-101 (one parabola, one
 These generators build B independent trajectories of the same loop with the geometry defined
 in DESIGN.md "reference paths":
   * spline  (config 2 / 4): natural cubic spline y(x) through 11 knots x in [-6, 34] m (4 m
-    spacing), y ~ U(-1, 1) m; linear extrapolation outside the knots.
+    spacing), y ~ U(-1, 1) m; linear extrapolation outside the knots.  Deviation from SURVEY.md
+    8(d) config 2 (6 knots on x in [0, 12]), deliberate: a trajectory starts at X in [-2, 2] and,
+    on the 0.8 -> 2.0 m/s ramp, covers about 17 m in the bench's 205 steps and 22 m in the dataset's
+    240 -- with knots on [0, 12] only, it would start on the extrapolated line and spend most of the
+    run past the last knot tracking a straight line (trivially easy QPs); the 4 m spacing keeps the
+    curvature of 6 knots over 12 m (2.4 m spacing) within a factor of 2.
   * mixed   (config 3): 50 % sinusoid y = A sin(w x + phase) (A = 0.5, w = 0.5 of MPC/README.md:75,
     jittered +-20 %), 50 % parabola y = a x^2 (a = 0.1 of main.py:64-66, drawn in [0.05, 0.15]).
 Initial state per trajectory (ranges of generation_type1.py:260-265 / main.py:77): X ~ U(-2, 2),
