@@ -79,6 +79,107 @@ def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):
                        f"{dt:.2f} s")
 
 
+def _config1_cases():
+    """BASELINE.json configs[0] and MPC/main.py's own loop, as (name, N, Ts, x0, u0, vref, path).
+    path: (kind, pcs, knots) of the trajectory's reference (PathSet / oracle kinds)."""
+    from trajectory_generation_amd.workload import make_workload as mk
+    w = mk(1, 20, 0.05, kind="spline", seed=0, id_offset=0)
+    main_x0 = np.array([0.0, 0.5, 0.0, 1.0, 0.0, 0.0])                       # MPC/main.py:80
+    main_u0 = np.array([TB.d_steady_state(1.0), 0.0])                          # MPC/main.py:21-22
+    return [
+        ("configs[0]: one spline trajectory, N=20, dt=0.05", 20, 0.05, w["x0"][0], w["u0"][0], w["vref"],
+         (int(w["kinds"][0]), np.asarray(w["pcs"][0], np.float64), w["knots"][0])),
+        ("MPC/main.py:72-101: parabola y = 0.1 x^2, N=40, Ts=0.02, ramp vref", 40, 0.02, main_x0, main_u0,
+         TB.vref_ramp(40, 0.02), (0, np.array([0.0, 0.0, 0.1, 0.0]), None)),
+    ]
+
+
+def _host_window(path, x_start, N, Ts, vref):
+    """MPC/main.py:51-68 on the host for one trajectory: the window the drop-in caller hands mpc_step."""
+    from trajectory_generation_amd.workload import spline_eval
+    kind, pc, kn = path
+    xs = np.zeros(N + 1)
+    xs[0] = x_start
+    for k in range(N):
+        xs[k + 1] = xs[k] + vref[k] * Ts
+    if kind == 0:
+        ys = pc[0] + xs * (pc[1] + xs * (pc[2] + xs * pc[3]))
+        dy = pc[1] + xs * (2.0 * pc[2] + xs * 3.0 * pc[3])
+    else:
+        coef = TB.spline_natural(kn[0], kn[1])
+        yd = [spline_eval(np.asarray(kn[0], np.float64), coef, x) for x in xs]
+        ys, dy = np.array([a for a, _ in yd]), np.array([b for _, b in yd])
+    return np.stack([xs, ys, np.arctan(dy)], axis=1)
+
+
+def config1_measure(dev, T=600, cpu=True):
+    """BASELINE.json configs[0] (one trajectory, the reference plumbing) on the GPU, three ways:
+      dropin  MPC/main.py's loop unchanged after the import swap -- per step the host window, the drop-in
+              mpc_step (one QP per call: host -> device copies, the launches, a synchronizing copy back) and
+              the drop-in f_cont for the Euler plant; per-call latency of mpc_step and loop steps/s;
+      fused   run_closed_loop at B = 1: the T steps in one launch (warm start as the headline, and cold);
+      cpu     the C oracle's closed loop on ONE thread, same T steps."""
+    from trajectory_generation_amd import mpc_6stati as M
+    out = []
+    for name, N, Ts, x0, u0, vref, path in _config1_cases():
+        rec = {"case": name, "steps": T}
+        # --- drop-in loop (MPC/main.py:85-101 with the drop-in module's mpc_step / f_cont)
+        for _ in range(3):   # warm the launch path (code objects, allocator)
+            M.mpc_step(x0, u0, _host_window(path, x0[0], N, Ts, vref), Ts=Ts, N=N, vref=vref)
+        x, u_prev = np.array(x0, np.float64), np.array(u0, np.float64)
+        lat, stats = [], []
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(T):
+            pr = _host_window(path, x[0], N, Ts, vref)
+            c0 = time.perf_counter()
+            u_cmd, status, _ = M.mpc_step(x, u_prev, pr, Ts=Ts, N=N, params=M.Params, vref=vref)
+            lat.append(time.perf_counter() - c0)
+            stats.append(status)
+            x = x + Ts * M.f_cont(x, u_cmd, M.Params)
+            u_prev = u_cmd
+        dt = time.perf_counter() - t0
+        lat = np.array(lat) * 1e6
+        rec["dropin"] = {"steps_per_s": T / dt, "mpc_step_us_median": float(np.median(lat)),
+                         "mpc_step_us_p99": float(np.percentile(lat, 99)),
+                         "loop_us_per_step": 1e6 * dt / T,
+                         "optimal_frac": float(np.mean([s == "optimal" for s in stats])), "final_x": x.tolist()}
+        # --- the same closed loop in one fused launch (B = 1)
+        kind, pc, kn = path
+        paths = TB.PathSet.build([kind], [pc], [kn], device=dev)
+        for ws_, key in ((1, "fused"), (0, "fused_cold")):
+            cfg = TB.config_struct(N=N, Ts=Ts, warm_start=ws_)
+            TB.run_closed_loop(x0, u0, paths, vref, T, cfg)            # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res = TB.run_closed_loop(x0, u0, paths, vref, T, cfg)
+            torch.cuda.synchronize()
+            dtf = time.perf_counter() - t0
+            rec[key] = {"steps_per_s": T / dtf, "us_per_step": 1e6 * dtf / T,
+                        "iters_mean": float(res["iters"].float().mean()),
+                        "final_x": res["X"][0, -1].cpu().numpy().tolist()}
+        if cpu:
+            rec["cpu_baseline"] = cpu_baseline_config1(N, Ts, x0, u0, vref, path, T)
+        out.append(rec)
+    return {"what": "BASELINE.json configs[0] / MPC/main.py on one trajectory: the drop-in per-call path, the "
+                    "fused closed loop at B=1, and the C oracle on 1 thread", "cases": out}
+
+
+def cpu_baseline_config1(N, Ts, x0, u0, vref, path, T):
+    """The oracle's closed loop (oracle/, C restatement of the reference path) for one trajectory, 1 thread."""
+    import oracle as O  # test infrastructure: used here only for the CPU-baseline leg
+    O.build()
+    kind, pc, kn = path
+    p = (O.Path(2, (0, 0, 0, 0), xk=kn[0], coef=TB.spline_natural(kn[0], kn[1]).reshape(-1)) if kind == 2
+         else O.Path(int(kind), pc))
+    cfg = O.cfg(N=N, Ts=Ts)
+    t0 = time.perf_counter()
+    r = O.closed_loop(p, x0, u0, vref, T, cfg)
+    dt = time.perf_counter() - t0
+    return {"steps_per_s": T / dt, "us_per_step": 1e6 * dt / T, "cores": 1, "kind": "port",
+            "iters_mean": float(np.mean(r["iters"])), "final_x": r["X"][-1].tolist()}
+
+
 # KalmanNet (BASELINE.json configs[4]): 1024 sequences x 200 steps, Ts = 0.01, float32
 KNET_FLOP_PER_SEQ_STEP = 2 * 3_178_373     # MACs of one gain-network step (SURVEY.md 8(a) a15) x 2
 FP32_MFMA_PEAK_TFS = 157.3                 # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
@@ -350,6 +451,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-steps", type=int, default=128)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-knet", action="store_true", help="skip the KalmanNet measurement (configs[4])")
+    ap.add_argument("--no-config1", action="store_true",
+                    help="skip the one-trajectory measurement (configs[0]: drop-in per call, fused B=1, oracle 1 thread)")
     ap.add_argument("--per-step", action="store_true",
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
     ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r02.json"),
@@ -554,6 +657,8 @@ def bench_run(args, ops, dist, rank, world):
         out["cpu_baseline"] = None
     if not args.no_knet and world == 1:
         out["knet"] = knet_measure(ops.dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json)
+    if not args.no_config1 and world == 1:
+        out["config1"] = config1_measure(ops.dev, cpu=not args.no_cpu)
     return out
 
 
