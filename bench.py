@@ -195,7 +195,8 @@ def knet_fc2_flop(B, model):
 
 
 def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
-                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r01.json")):
+                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r01.json"), weights=None,
+                 trained_json=os.path.join(HERE, "profiles", "r03_knet_trained_mse.json")):
     """Sequences/s of KalmanNet inference (BASELINE.json configs[4]) on 1024 noisy closed-loop
     trajectories x 200 steps at Ts = 0.01 generated on the GPU (knet_eval.make_sequences: the dataset
     emitter's closed loop + the reference's measurement noise), normalization and clamp limits from a
@@ -215,6 +216,9 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
     model = K.KalmanNetNN(dev)
     model.NNBuild(sysm, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128)
     model.set_normalization(xm, xs, ym, ys)
+    if weights:   # trained weights (tools/knet_train_eval.py --save): the MSE then compares a trained filter
+        from safetensors.torch import load_file
+        model.load_state_dict({k: v.to(dev) for k, v in load_file(weights).items()})
     model.eval()
     y = ((test["y"] - ym) / ys).contiguous()
     u = test["u"].contiguous()
@@ -271,7 +275,9 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
                       "Ts": Ts},
            "mse": knet_mse, "mse_db": knet_db, "mse_module_path": mod_mse, "ekf_mse": ekf_mse, "ekf_mse_db": ekf_db,
            "mse_note": "test_vehicle.py:15-40/149-158 loss on the same 1024 x 200 measurements; KalmanNet weights "
-                       "are the seeded init (no trained weights ship), the EKF is the build's baseline (f2)",
+                       + (f"from {os.path.basename(weights)}" if weights else
+                          "are the seeded init (no trained weights ship; see 'mse_trained')")
+                       + ", the EKF is the build's baseline (f2)",
            "roofline": {"bound": "mfma", "achieved": fc2_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": fc2_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
                         "kernel": "knet_fc2_kernel<5> (FC2: Linear 256->10240, ReLU, Linear 10240->30)",
@@ -279,6 +285,15 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
                         "traffic_source": os.path.relpath(traffic_json, HERE) if traffic is not None else None,
                         "whole_step": {"achieved": achieved, "frac": achieved / FP32_MFMA_PEAK_TFS,
                                        "flop_per_seq_step": KNET_FLOP_PER_SEQ_STEP}}}
+    if os.path.exists(trained_json):
+        # the trained network's MSE on this same test draw, recorded by tools/knet_train_eval.py
+        try:
+            with open(trained_json) as f:
+                tr = json.load(f)
+            out["mse_trained"] = dict(tr["test"], source=os.path.relpath(trained_json, HERE),
+                                      training=tr.get("training", {}).get("steps"))
+        except (OSError, ValueError, KeyError):
+            pass
     if cpu:
         import oracle.knet_oracle as KO  # test infrastructure: CPU-baseline leg only
         w = {k: v.detach().cpu() for k, v in model.state_dict().items()}
@@ -397,7 +412,9 @@ def dataset_leg(args, w, ops, dist, rank, world):
     """BASELINE.json configs[3] on this node: every rank runs the closed loop of its --batch trajectories
     (ids rank * B + i, the bench workload) for --dataset-steps steps from the initial states, the packed
     [B, T+1, 9] histories go to rank 0 with one dist.gather (RCCL over xGMI), and rank 0 optionally
-    writes the CSVs.  Generation, gather and CSV writing are timed separately (max over ranks)."""
+    writes the CSVs (+ the status sidecar).  With --dataset-csv the per-rank alternative (SURVEY.md 8(e):
+    every rank writes its own shard, no gather) is timed beside it.  Generation, gather and CSV writing are
+    timed separately (max over ranks)."""
     from trajectory_generation_amd import dataset as D
     B, N, Ts, T = args.batch, args.horizon, args.dt, args.dataset_steps
 
@@ -406,6 +423,12 @@ def dataset_leg(args, w, ops, dist, rank, world):
         if dist:
             dist.barrier()
         ops.sync()
+
+    def tmax(v):
+        t = torch.tensor([v], dtype=torch.float64, device=ops.dev)
+        if dist:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
     bar()
     t0 = time.perf_counter()
@@ -416,25 +439,34 @@ def dataset_leg(args, w, ops, dist, rank, world):
     full = D.gather_to_root(blk, dist)
     bar()
     t2 = time.perf_counter()
-    times = torch.tensor([t1 - t0, t2 - t1], dtype=torch.float64, device=ops.dev)
-    if dist:
-        dist.all_reduce(times, op=dist.ReduceOp.MAX)
-    gen_s, gather_s = (float(v) for v in times.cpu())
-    if rank != 0:
-        return None
-    X, U, st = D.unpack_history(full)
-    csv_s = None
+    gen_s, gather_s = tmax(t1 - t0), tmax(t2 - t1)
+    csv_s = shard_s = None
     if args.dataset_csv:
         os.makedirs(args.dataset_csv, exist_ok=True)
-        t3 = time.perf_counter()
-        D.write_csv(os.path.join(args.dataset_csv, "vehicle_mpc"), X.cpu().numpy(), U.cpu().numpy(),
-                    np.arange(X.shape[0]), Ts)
-        csv_s = time.perf_counter() - t3
+        if rank == 0:
+            Xa, Ua, sta = D.unpack_history(full)
+            t3 = time.perf_counter()
+            D._write_with_sidecar(os.path.join(args.dataset_csv, "vehicle_mpc"), Xa, Ua, sta, np.arange(Xa.shape[0]),
+                                  Ts, False)
+            csv_s = time.perf_counter() - t3
+        bar()
+        t4 = time.perf_counter()
+        D._write_with_sidecar(os.path.join(args.dataset_csv, f"vehicle_mpc_rank{rank}"), X, U, status,
+                              np.arange(rank * B, rank * B + B), Ts, False)
+        shard_s = tmax(time.perf_counter() - t4)
+    if rank != 0:
+        return None
+    Xa, Ua, st = D.unpack_history(full)
+    stn = st.cpu().numpy()
     n = world * B * T
     return {"what": "configs[3]: closed-loop dataset generation, histories gathered into rank 0",
             "trajectories": world * B, "steps": T, "traj_steps_per_s": n / gen_s, "generate_s": gen_s,
             "gather_s": gather_s, "gather_bytes": int(full.numel() * full.element_size()),
-            "csv_s": csv_s, "status_hist": torch.bincount(st.reshape(-1).long(), minlength=7).tolist()}
+            "csv_s": csv_s, "csv_shards_s": shard_s,
+            "csv_note": "csv_s: rank 0 writes the gathered CSVs + status sidecar; csv_shards_s: every rank writes "
+                        "its own shard (no gather), max over ranks" if args.dataset_csv else None,
+            "status_hist": np.bincount(stn.reshape(-1).astype(np.int64), minlength=7).tolist(),
+            "failed_trajectories": int(((stn >= D.FAILED_STATUS).sum(axis=0) > 0).sum())}
 
 
 def parse_args(argv=None):
@@ -461,6 +493,8 @@ def parse_args(argv=None):
                     help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
     ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r01.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
+    ap.add_argument("--knet-weights", default=None,
+                    help="safetensors of trained KalmanNet weights (tools/knet_train_eval.py --save) for configs[4]")
     ap.add_argument("--dataset-steps", type=int, default=240,
                     help="configs[3] leg: closed-loop dataset generation of --batch trajectories per GPU over this "
                          "many steps, then the histories gathered into rank 0 (0 disables)")
@@ -656,7 +690,8 @@ def bench_run(args, ops, dist, rank, world):
     else:
         out["cpu_baseline"] = None
     if not args.no_knet and world == 1:
-        out["knet"] = knet_measure(ops.dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json)
+        out["knet"] = knet_measure(ops.dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json,
+                                   weights=args.knet_weights)
     if not args.no_config1 and world == 1:
         out["config1"] = config1_measure(ops.dev, cpu=not args.no_cpu)
     return out

@@ -65,20 +65,21 @@ def _free_port():
     return p
 
 
-def _rank(rank, port, q):
+def _rank(rank, port, q, csv_dir):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import bench
     out = bench.main(["--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "4", "--dataset-steps", "5",
-                      "--no-cpu", "--no-knet", "--dist-timeout", "120"], ops_factory=CpuOps, backend="gloo")
+                      "--no-cpu", "--no-knet", "--dist-timeout", "120", "--dataset-csv", csv_dir],
+                     ops_factory=CpuOps, backend="gloo")
     q.put((rank, out))
 
 
-def test_bench_run_two_ranks_gloo():
+def test_bench_run_two_ranks_gloo(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, port, q, str(tmp_path))) for r in range(2)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=180) for _ in range(2))
@@ -93,7 +94,14 @@ def test_bench_run_two_ranks_gloo():
     assert out["cold"]["iters_mean"] == 50.0 and out["solver_stats"]["iters_mean"] == 25.0
     ds = out["dataset"]
     assert ds["trajectories"] == 8 and ds["steps"] == 5 and ds["gather_bytes"] == 8 * 6 * 9 * 8
-    assert ds["status_hist"][0] == 8 * 5
+    assert ds["status_hist"][0] == 8 * 5 and ds["failed_trajectories"] == 0
+    # the gathered files on rank 0 and one shard per rank (ids 0-3, 4-7), each with its status sidecar
+    assert ds["csv_s"] is not None and ds["csv_shards_s"] is not None
+    one = open(tmp_path / "vehicle_mpc_clean.csv").read().splitlines()
+    sh = [open(tmp_path / f"vehicle_mpc_rank{r}_clean.csv").read().splitlines() for r in range(2)]
+    assert sh[0][1:] + sh[1][1:] == one[1:] and len(one) == 1 + 8 * 6
+    for r in range(2):
+        assert len(open(tmp_path / f"vehicle_mpc_rank{r}_status.csv").read().splitlines()) == 5
 
 
 def test_spawned_worker_failure_stops_the_siblings():

@@ -58,14 +58,16 @@ def _fake_closed_loop(w, T, cfg):
     return dict(X=X, U=U, status=st)
 
 
-def _worker(rank, world, port, q, out_prefix):
+def _worker(rank, world, port, q, out_prefix, shards=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     B, T = 4, 6
     r = D.generate(B, T, N=20, Ts=0.05, kind="spline", seed=3, out_prefix=out_prefix, dist=dist,
-                   closed_loop=_fake_closed_loop)
-    if rank == 0:
+                   closed_loop=_fake_closed_loop, shards=shards)
+    if shards:
+        q.put((rank, r[0].numpy(), r[1].numpy(), r[2].numpy()))
+    elif rank == 0:
         X, U, st = r
         q.put((X.numpy(), U.numpy(), st.numpy()))
     else:
@@ -105,6 +107,79 @@ def test_generate_two_ranks_gloo(tmp_path):
     assert sorted(clean["trajectory_id"].unique()) == list(range(8))
     assert len(clean) == 8 * 7 and len(noisy) == 8 * 7
     np.testing.assert_allclose(clean["X"].to_numpy().reshape(8, 7), gX[:, :, 0], rtol=0, atol=1e-12)
+
+
+def test_generate_two_ranks_per_rank_shards_gloo(tmp_path):
+    """shards=True (SURVEY.md 8(e)'s per-rank alternative): no gather, each rank writes its own CSV shard and
+    status sidecar with the global ids; the shards' bodies concatenated in rank order are byte for byte the
+    single gathered file's body."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    prefix = str(tmp_path / "sh")
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, prefix, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted([q.get(timeout=120) for _ in range(2)], key=lambda g: g[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    X = np.concatenate([g[1] for g in got])
+    U = np.concatenate([g[2] for g in got])
+    st = np.concatenate([g[3] for g in got], axis=1)
+    D.write_csv(str(tmp_path / "one"), X, U, np.arange(8), 0.05)
+    D.write_status_csv(str(tmp_path / "one"), st, np.arange(8))
+    for part in ("clean", "noisy", "status"):
+        one = open(tmp_path / f"one_{part}.csv").read().splitlines()
+        shards = [open(f"{prefix}_rank{r}_{part}.csv").read().splitlines() for r in range(2)]
+        assert shards[0][0] == shards[1][0] == one[0]
+        assert shards[0][1:] + shards[1][1:] == one[1:]
+
+
+def _status_closed_loop(w, T, cfg):
+    """Stand-in with chosen statuses: trajectory 2 fails at step 1 (solver error), 4 at step 3 (iteration
+    limit, status 2); everything else optimal / optimal_inaccurate."""
+    r = _fake_closed_loop(w, T, cfg)
+    st = torch.zeros((T, len(w["ids"])), dtype=torch.int32)
+    st[0, 1] = 1
+    st[1, 2] = 6
+    st[3, 4] = 2
+    r["status"] = st
+    return r
+
+
+def test_status_sidecar_and_failed_trajectory_filter(tmp_path):
+    """The reference's CSV schema carries no status: generate writes {prefix}_status.csv beside it (worst
+    status, failed-step count, first failed step per trajectory) and, with drop_failed, leaves out the
+    trajectories with a failed step and re-indexes the rest 0..n-1 (the ids data_loader.py reads), each
+    keeping the noise draw of its generation id."""
+    import pandas as pd
+    B, T = 6, 4
+    p1 = str(tmp_path / "all")
+    X, U, st = D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p1, closed_loop=_status_closed_loop)
+    sc = pd.read_csv(p1 + "_status.csv")
+    assert list(sc.columns) == ["trajectory_id", "source_id", "worst_status", "n_failed_steps", "first_failed_step"]
+    assert sc["worst_status"].tolist() == [0, 1, 6, 0, 2, 0]
+    assert sc["n_failed_steps"].tolist() == [0, 0, 1, 0, 1, 0]
+    assert sc["first_failed_step"].tolist() == [-1, -1, 1, -1, 3, -1]
+    assert list(pd.read_csv(p1 + "_clean.csv").columns) == D.CLEAN_COLUMNS   # schema unchanged
+    p2 = str(tmp_path / "ok")
+    D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p2, closed_loop=_status_closed_loop, drop_failed=True)
+    sc2 = pd.read_csv(p2 + "_status.csv")
+    assert sc2["trajectory_id"].tolist() == [0, 1, 2, 3] and sc2["source_id"].tolist() == [0, 1, 3, 5]
+    assert (sc2["n_failed_steps"] == 0).all()
+    clean = pd.read_csv(p2 + "_clean.csv")
+    noisy = pd.read_csv(p2 + "_noisy.csv")
+    assert sorted(clean["trajectory_id"].unique()) == [0, 1, 2, 3]
+    Xn = X.numpy()
+    keep = [0, 1, 3, 5]
+    np.testing.assert_array_equal(clean["X"].to_numpy().reshape(4, T + 1), Xn[keep, :, 0])
+    noise = np.stack([D.measurement_noise(i, T + 1)[:, 0] for i in keep])
+    np.testing.assert_allclose(noisy["X"].to_numpy().reshape(4, T + 1), Xn[keep, :, 0] + noise, rtol=0, atol=1e-12)
+    res = D.load_vehicle_dataset(p2 + "_noisy.csv", p2 + "_clean.csv", T_steps=T + 1, train_split=0.5, val_split=0.25)
+    assert res is not None and sum(part[0].shape[0] for part in res) == 4
+    with pytest.raises(ValueError):
+        D.generate(B, T, out_prefix=p2, closed_loop=_status_closed_loop, drop_failed=True, shards=True)
 
 
 def test_pack_unpack_history():

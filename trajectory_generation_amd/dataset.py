@@ -34,15 +34,16 @@ def measurement_noise(traj_id: int, n_rows: int, stds=None, seed_base=NOISE_SEED
     return np.column_stack([rng.normal(0, s[k], n_rows) for k in ("X", "Y", "phi", "vx", "vy", "omega")])
 
 
-def frames(X, U, ids, Ts):
+def frames(X, U, ids, Ts, noise_ids=None):
     """X [B,T+1,6], U [B,T,2] (numpy), ids [B] -> (clean, noisy) pandas DataFrames in the reference
-    column order, trajectories stacked in id order."""
+    column order, trajectories stacked in id order.  noise_ids: the ids whose noise draws are added
+    (default ids; differs when a filtered dataset is re-indexed)."""
     import pandas as pd
     X = np.asarray(X, dtype=np.float64)
     U = np.asarray(U, dtype=np.float64)
     B, n_rows = X.shape[0], X.shape[1]
     t = np.arange(n_rows) * Ts
-    Xn = X + np.stack([measurement_noise(i, n_rows) for i in ids])
+    Xn = X + np.stack([measurement_noise(i, n_rows) for i in (ids if noise_ids is None else noise_ids)])
     dU = np.concatenate([U, np.full((B, 1, 2), np.nan)], axis=1)
     tid = np.repeat(np.asarray(ids, dtype=np.int64), n_rows)
     tt = np.tile(t, B)
@@ -97,6 +98,35 @@ def gather_to_root(blk, dist=None, dst=0):
     return None
 
 
+FAILED_STATUS = 2   # statuses >= 2 (solver error, infeasible, iteration limit, ...): the step kept u_prev
+
+
+def status_summary(status, ids):
+    """status [T,B] (the closed loop's per-step solver status) -> per trajectory (ids [B]): the worst
+    status, the number of failed steps (status >= 2) and the first failed step (-1 if none)."""
+    st = np.asarray(status)
+    T = st.shape[0]
+    failed = st >= FAILED_STATUS
+    n_failed = failed.sum(axis=0)
+    first = np.where(n_failed > 0, np.argmax(failed, axis=0), -1) if T else np.full(st.shape[1], -1)
+    worst = st.max(axis=0) if T else np.zeros(st.shape[1], dtype=st.dtype)
+    return {"trajectory_id": np.asarray(ids, dtype=np.int64), "worst_status": worst.astype(np.int64),
+            "n_failed_steps": n_failed.astype(np.int64), "first_failed_step": first.astype(np.int64)}
+
+
+def write_status_csv(out_prefix, status, ids, source_ids=None):
+    """``{out_prefix}_status.csv`` beside the dataset CSVs (whose reference schema stays unchanged): one row
+    per written trajectory -- trajectory_id, source_id (the generation id; differs after filtering),
+    worst_status, n_failed_steps, first_failed_step."""
+    sm = status_summary(status, source_ids if source_ids is not None else ids)
+    with open(f"{out_prefix}_status.csv", "w") as f:
+        f.write("trajectory_id,source_id,worst_status,n_failed_steps,first_failed_step\n")
+        for i, src, w, n, fs in zip(np.asarray(ids, np.int64), sm["trajectory_id"], sm["worst_status"],
+                                    sm["n_failed_steps"], sm["first_failed_step"]):
+            f.write(f"{i},{src},{w},{n},{fs}\n")
+    return sm
+
+
 def _closed_loop_gpu(w, T, cfg):
     """This rank's closed loop on the GPU (batch.run_closed_loop, fused launch)."""
     from . import batch as TB
@@ -105,13 +135,22 @@ def _closed_loop_gpu(w, T, cfg):
 
 
 def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=None, polish_mode=0,
-             closed_loop=None):
+             closed_loop=None, drop_failed=False, shards=False):
     """Run the closed loop for this rank's B trajectories (ids rank * B .. rank * B + B - 1), gather the
-    histories to rank 0 and (rank 0) write ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv``.
+    histories to rank 0 and (rank 0) write ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` and the
+    status sidecar ``{out_prefix}_status.csv`` (write_status_csv).
 
+    drop_failed: leave out every trajectory with a failed step (status >= 2) and re-index the rest 0..n-1 (the
+      ids data_loader.py expects, merge_datasets.py's re-indexing) -- each keeps the noise of its generation
+      id, which the sidecar's source_id column records.  Default False: every trajectory is written, the
+      sidecar flags the failed ones.
+    shards: no gather -- every rank writes its own ``{out_prefix}_rank{r}_*.csv`` (global ids; the shards'
+      bodies concatenated in rank order are the single file's body) and its sidecar (SURVEY.md 8(e)'s
+      per-rank alternative); returns this rank's share on every rank.
     closed_loop(workload, T, cfg) -> dict(X, U, status) runs one rank's share (default: the fused GPU
     closed loop); tests inject a CPU stand-in to exercise the id offsets and the gather.
-    Returns (X [W B,T+1,6], U [W B,T,2], status [T,W B]) on rank 0 and None on the other ranks."""
+    Returns (X [W B,T+1,6], U [W B,T,2], status [T,W B]) on rank 0 and None on the other ranks (shards:
+    this rank's (X, U, status) everywhere)."""
     from .workload import make_workload
     rank = dist.get_rank() if (dist is not None and dist.is_initialized()) else 0
     w = make_workload(B, N, Ts, kind=kind, seed=seed, id_offset=rank * B)
@@ -120,24 +159,48 @@ def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=N
         from . import batch as TB
         cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
         closed_loop = _closed_loop_gpu
+    if shards and drop_failed:
+        raise ValueError("drop_failed re-indexes the whole dataset: it needs the gather (shards=False)")
     res = closed_loop(w, T, cfg)
+    if shards:
+        X, U, st = res["X"], res["U"], res["status"]
+        if out_prefix is not None:
+            _write_with_sidecar(f"{out_prefix}_rank{rank}", X, U, st, np.arange(rank * B, rank * B + B), Ts,
+                                drop_failed)
+        return X, U, st
     blk = gather_to_root(pack_history(res["X"], res["U"], res["status"]), dist)
     if blk is None:
         return None
     X, U, st = unpack_history(blk)
     if out_prefix is not None:
-        write_csv(out_prefix, X.cpu().numpy(), U.cpu().numpy(), np.arange(X.shape[0]), Ts)
+        _write_with_sidecar(out_prefix, X, U, st, np.arange(X.shape[0]), Ts, drop_failed)
     return X, U, st
 
 
-def write_csv(out_prefix, X, U, ids, Ts, native=True, nthreads=None):
+def _write_with_sidecar(prefix, X, U, st, ids, Ts, drop_failed):
+    """CSVs + status sidecar of trajectories `ids` (generation ids); drop_failed re-indexes the kept ones."""
+    Xh, Uh = X.cpu().numpy() if hasattr(X, "cpu") else X, U.cpu().numpy() if hasattr(U, "cpu") else U
+    sth = st.cpu().numpy() if hasattr(st, "cpu") else np.asarray(st)
+    ids = np.asarray(ids, dtype=np.int64)
+    if drop_failed:
+        keep = np.nonzero((sth >= FAILED_STATUS).sum(axis=0) == 0)[0]
+        out_ids = np.arange(keep.size, dtype=np.int64)
+        write_csv(prefix, Xh[keep], Uh[keep], out_ids, Ts, noise_ids=ids[keep])
+        write_status_csv(prefix, sth[:, keep], out_ids, source_ids=ids[keep])
+    else:
+        write_csv(prefix, Xh, Uh, ids, Ts)
+        write_status_csv(prefix, sth, ids)
+
+
+def write_csv(out_prefix, X, U, ids, Ts, native=True, nthreads=None, noise_ids=None):
     """``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` in the reference schema (see frames).
     native: the library's multi-threaded writer (traj_dataset_write_csv), byte-identical to the pandas
-    writer (native=False, frames + DataFrame.to_csv)."""
+    writer (native=False, frames + DataFrame.to_csv).  noise_ids: see frames."""
     X = np.ascontiguousarray(X, dtype=np.float64)
     U = np.ascontiguousarray(U, dtype=np.float64)
+    nids = ids if noise_ids is None else noise_ids
     if not native:
-        clean, noisy = frames(X, U, ids, Ts)
+        clean, noisy = frames(X, U, ids, Ts, noise_ids=noise_ids)
         clean.to_csv(f"{out_prefix}_clean.csv", index=False)
         noisy.to_csv(f"{out_prefix}_noisy.csv", index=False)
         return
@@ -145,7 +208,7 @@ def write_csv(out_prefix, X, U, ids, Ts, native=True, nthreads=None):
     import os
     from . import _lib
     B, n_rows = X.shape[0], X.shape[1]
-    noise = np.ascontiguousarray(np.stack([measurement_noise(i, n_rows) for i in ids]) if B else
+    noise = np.ascontiguousarray(np.stack([measurement_noise(i, n_rows) for i in nids]) if B else
                                  np.zeros((0, n_rows, 6)))
     ids64 = np.ascontiguousarray(ids, dtype=np.int64)
     nt = int(nthreads or min(16, os.cpu_count() or 1))

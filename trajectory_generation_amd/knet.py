@@ -617,3 +617,7 @@ def ekf_run(params: dict, Ts: float, y, u, x0, P0=EKF_P0, Q=EKF_Q, R=EKF_R):
                                            B, T, _p(yy), _p(uu), _p(xx), _p(p0), _p(q), _p(r), _p(out),
                                            _stream()), "traj_ekf_run_f64")
     return out
+
+
+# torch.ops.trajknet.* (prior, gru_gates, update, pack, step): the same HIP ops registered with torch.library
+from . import knet_ops  # noqa: E402,F401

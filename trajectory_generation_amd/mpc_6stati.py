@@ -25,6 +25,8 @@ succeeds; see DESIGN.md "Parity" for the stated tolerances.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
 import torch
 
@@ -44,6 +46,54 @@ def _np(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy()
 
 
+class _CallIO:
+    """Pinned host staging for the one-trajectory calls of this module (the reference's call shape): the inputs
+    go to the device in ONE copy, the kernel writes every output into ONE device buffer, and ONE copy back plus
+    one stream synchronization ends the call -- instead of a copy per argument and a synchronizing read per
+    output.  Per (device, stream, N); reused across calls (each call synchronizes before it returns)."""
+
+    _cache: dict = {}
+
+    def __init__(self, dev, nin: int, nf: int, ni: int):
+        self.h_in = torch.empty(nin, dtype=torch.float64, pin_memory=True)
+        self.d_in = torch.empty(nin, dtype=torch.float64, device=dev)
+        nio = nf + (ni + 1) // 2          # int32 outputs packed after the doubles
+        self.nf = nf
+        self.d_out = torch.empty(nio, dtype=torch.float64, device=dev)
+        self.h_out = torch.empty(nio, dtype=torch.float64, pin_memory=True)
+        self.a_in = self.h_in.numpy()
+        self.a_out = self.h_out.numpy()
+
+    @classmethod
+    def get(cls, key, dev, nin, nf, ni):
+        k = (str(dev), torch.cuda.current_stream(dev).cuda_stream) + tuple(key)
+        io = cls._cache.get(k)
+        if io is None:
+            io = cls._cache[k] = cls(dev, nin, nf, ni)
+        return io
+
+    def send(self):
+        self.d_in.copy_(self.h_in, non_blocking=True)
+
+    def receive(self):
+        self.h_out.copy_(self.d_out, non_blocking=True)
+        torch.cuda.current_stream(self.d_out.device).synchronize()
+        return self.a_out
+
+
+_PSD_CACHE: dict = {}
+
+
+def _is_psd_cached(M: np.ndarray) -> bool:
+    k = (M.shape, M.tobytes())
+    v = _PSD_CACHE.get(k)
+    if v is None:
+        if len(_PSD_CACHE) > 64:
+            _PSD_CACHE.clear()
+        v = _PSD_CACHE[k] = _is_psd(M)
+    return v
+
+
 def tire_forces(x, u, p):
     """(Fy_f, Fy_r, Frx) at x (6,), u (2,) -- mpc_6stati.py:25-53 (HIP kernel)."""
     out = _np(_b.tire_forces_batch(np.asarray(x, np.float64).reshape(1, 6), np.asarray(u, np.float64).reshape(1, 2),
@@ -53,8 +103,17 @@ def tire_forces(x, u, p):
 
 def f_cont(x, u, p):
     """Continuous-time dynamics f(x,u) -> ndarray (6,) -- mpc_6stati.py:55-71 (HIP kernel)."""
-    return _np(_b.f_cont_batch(np.asarray(x, np.float64).reshape(1, 6), np.asarray(u, np.float64).reshape(1, 2),
-                               p))[0]
+    x = np.asarray(x, np.float64).reshape(6)
+    u = np.asarray(u, np.float64).reshape(2)
+    dev = _b.require_gpu()
+    io = _CallIO.get(("f_cont",), dev, 8, 6, 0)
+    io.a_in[:6] = x
+    io.a_in[6:] = u
+    io.send()
+    _b._lib.check(_b._lib.lib().traj_f_cont_batch(C.byref(_b.params_struct(p)), 1, _b._p(io.d_in),
+                                                  C.c_void_p(io.d_in.data_ptr() + 48), _b._p(io.d_out), _b._stream()),
+                  "traj_f_cont_batch")
+    return io.receive()[:6].copy()
 
 
 def numerical_jacobian(f, x, u, p, eps_x=1e-5, eps_u=1e-5):
@@ -138,25 +197,42 @@ def mpc_step(
         vref = np.asarray(vref).reshape(N + 1)
     R = np.asarray(R, dtype=np.float64)
     Rd = np.asarray(Rd, dtype=np.float64)
-    if not (_is_psd(R) and _is_psd(Rd)):
+    if not (_is_psd_cached(R) and _is_psd_cached(Rd)):
         # cvxpy rejects a non-convex quad_form at prob.solve (inside the reference's try, :255-259)
         return u_pr, "Solver Error: DCPError", {}
     cfg = _b.config_struct(N=N, Ts=Ts, q_c=q_c, q_phi=q_phi, q_vx=q_vx, R=R, Rd=Rd, u_bounds=u_bounds,
                            du_bounds=du_bounds, x_lo=x_lo, x_hi=x_hi, **solver_settings)
-    o = _b.mpc_step_batch(x0.reshape(1, 6), u_pr.reshape(1, 2), path_ref.astype(np.float64).reshape(1, N + 1, 3),
-                          vref.astype(np.float64).reshape(1, N + 1), cfg, p)
-    st = int(o["status"][0].item())
+    # one staged copy in: [x0 6 | u_prev 2 | path_ref 3(N+1) | vref N+1]; one copy out:
+    # [u_cmd 2 | objective 1 | X_opt 6(N+1) | U_opt 2N | status, iters, polished (int32)]
+    dev = _b.require_gpu()
+    nin, nf = 8 + 4 * (N + 1), 3 + 6 * (N + 1) + 2 * N
+    io = _CallIO.get(("mpc_step", N), dev, nin, nf, 3)
+    a = io.a_in
+    a[:6] = x0
+    a[6:8] = u_pr
+    a[8:8 + 3 * (N + 1)] = np.asarray(path_ref, np.float64).reshape(-1)
+    a[8 + 3 * (N + 1):] = np.asarray(vref, np.float64).reshape(-1)
+    io.send()
+    d, do = io.d_in, io.d_out
+    ints = do[nf:].view(torch.int32)
+    out = {"u_cmd": do[0:2].view(1, 2), "objective": do[2:3], "X_opt": do[3:3 + 6 * (N + 1)].view(1, 6, N + 1),
+           "U_opt": do[3 + 6 * (N + 1):nf].view(1, 2, N), "status": ints[0:1], "iters": ints[1:2],
+           "polished": ints[2:3]}
+    _b.mpc_step_batch(d[:6].view(1, 6), d[6:8].view(1, 2), d[8:8 + 3 * (N + 1)].view(1, N + 1, 3),
+                      d[8 + 3 * (N + 1):].view(1, N + 1), cfg, p, out=out)
+    h = io.receive()
+    st = int(h[nf:].view(np.int32)[0])
     status = STATUS_STRINGS.get(st, "Solver Error: SolverError")
     if st == 6:
         return u_pr, status, {}
     if status not in ("optimal", "optimal_inaccurate"):
         return u_pr, status, {}
-    u_cmd = _np(o["u_cmd"])[0].reshape(2)
+    u_cmd = h[0:2].copy()
     info = {
         "status": status,
-        "objective": float(o["objective"][0].item()),
-        "X_opt": _np(o["X_opt"])[0],
-        "U_opt": _np(o["U_opt"])[0],
+        "objective": float(h[2]),
+        "X_opt": h[3:3 + 6 * (N + 1)].reshape(6, N + 1).copy(),
+        "U_opt": h[3 + 6 * (N + 1):nf].reshape(2, N).copy(),
         "path_ref": path_ref,
         "vref": vref,
     }
