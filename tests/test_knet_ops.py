@@ -143,5 +143,6 @@ def test_op_autograd_matches_module_functions(gpu):
     gb = torch.autograd.grad(K._GruGatesFn.apply(gi, gh, h), [gi, gh, h], [go])
     assert all(torch.equal(p, q) for p, q in zip(ga, gb))
     for op, args in ((torch.ops.trajknet.gru_gates.default, (f(B, 3 * H), f(B, 3 * H), f(B, H))),
-                     (torch.ops.trajknet.update.default, (f(B, 6), f(B, 30), f(B, 5), f(())))):
+                     (torch.ops.trajknet.update.default, (f(B, 6), f(B, 30), f(B, 5),
+                                                          torch.tensor(0.3, device=gpu)))):
         torch.library.opcheck(op, args, test_utils=("test_schema", "test_faketensor"))
