@@ -361,6 +361,8 @@ class GpuOps:
     def __init__(self, local: int):
         self.dev = TB.require_gpu(f"cuda:{local}")
         torch.cuda.set_device(self.dev)
+        if os.environ.get("TRAJ_FUSED_WAVES"):   # experiments: force the fused kernel instance (traj_debug_fused_waves)
+            _lib.check(_lib.lib().traj_debug_fused_waves(int(os.environ["TRAJ_FUSED_WAVES"])), "traj_debug_fused_waves")
 
     def sync(self):
         torch.cuda.synchronize()

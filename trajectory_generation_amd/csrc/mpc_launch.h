@@ -23,7 +23,8 @@ int launch_fused(const KArgs& a, hipStream_t st) {
                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, solve_kernel<NN, true, true, false, WPS>, (int)sblock.x, 0);
         if (e != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             return -3;
-        const int cap = 4 * WPS;   // one-wave workgroups: WPS per SIMD, 4 SIMDs
+        constexpr int WAVES = (NN + 63) / 64;
+        const int cap = 4 * WPS / WAVES;   // WPS waves per SIMD, 4 SIMDs, WAVES waves per workgroup
         slots_per_cu[diag][dev] = nb < 1 ? 1 : (nb > cap ? cap : nb);
         cus[dev] = ncu < 1 ? 1 : ncu;
     }

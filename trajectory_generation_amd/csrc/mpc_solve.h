@@ -41,6 +41,18 @@
 #ifndef TGMPC_PCH
 #define TGMPC_PCH 4            // CMP: pivot-row double2 per chunk of the sweep
 #endif
+#ifndef TGMPC_L2W_WPE
+#define TGMPC_L2W_WPE 2        // waves per SIMD the lean two-wave instance is built for
+#endif
+#ifndef TGMPC_KCH_W2
+#define TGMPC_KCH_W2 8         // fused one-wave instance at 2 waves per SIMD: broadcast values per mat-vec chunk (0: all)
+#endif
+#ifndef TGMPC_PCH_W2
+#define TGMPC_PCH_W2 4         // fused one-wave instance at 2 waves per SIMD: pivot-row double2 per chunk (0: all)
+#endif
+#ifndef TGMPC_PCH2
+#define TGMPC_PCH2 4           // L2W: pivot-row double2 per chunk of the two-wave sweep
+#endif
 
 namespace tgmpc {
 
@@ -66,8 +78,10 @@ __device__ __forceinline__ double ld_coh(const double* p) {
 // WPS: waves per SIMD the register allocation is held to (fused one-wave kernels: 2, or 3 -- 168 VGPRs, the
 // compact LDS image; mpc_inst_w3.hip).
 template <int NN, bool CLOSED, bool FUSED = false, bool DIAG = true, int WPS = 2>
-// (capacity 64: the row of K^-1 and its broadcast vector alone are 256 VGPRs -- one wave per SIMD)
-__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(NN <= 40 ? WPS : 1))) void solve_kernel(const KArgs a0) {
+// (capacity 64: the row of K^-1 and its broadcast vector alone are 256 VGPRs -- one wave per SIMD; capacity 80,
+// two waves per instance: one wave per SIMD, or, fused with WPS = 2, two -- the lean two-wave instance below)
+__global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(
+    NN <= 40 ? WPS : ((FUSED && NN > 64 && WPS >= 2) ? TGMPC_L2W_WPE : 1)))) void solve_kernel(const KArgs a0) {
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
@@ -79,33 +93,40 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr bool CMP = FUSED && WAVES == 1;
     // LEAN (the 3-wave instance): values parked in / re-formed from LDS around the factorization, a rolled P v
     // -- register savings the 2-wave instance does without (same arithmetic, same results)
-    constexpr bool LEAN = CMP && WPS >= 3;
-    __shared__ double s_pref0[CMP ? 2 : 3 * (NM + 1)];
-    __shared__ double s_vref0[CMP ? 2 : NM + 1];
+    // L2W (fused, two waves per instance at capacity 80, WPS = 2): 4 instances per CU instead of 2 -- 256
+    // registers per lane and <= 40 KB of LDS: cold rows of NN, the sweep's pivot columns in the exchange region,
+    // the window in s_big past the stage records, chunked pivot-row / broadcast reads and the LEAN parking
+    constexpr bool L2W = FUSED && WAVES == 2 && WPS >= 2;
+    constexpr bool LEAN = (CMP && WPS >= 3) || L2W;
+    static_assert(!L2W || CLOSED, "the lean two-wave instance is the fused closed loop");
+    __shared__ double s_pref0[(CMP || L2W) ? 2 : 3 * (NM + 1)];
+    __shared__ double s_vref0[(CMP || L2W) ? 2 : NM + 1];
     __shared__ double s_x0[6], s_up[2];
     __shared__ int s_item;
     // one region, two lives: A_k, B_k, g_k of every stage staged for the condensing (fused: stage records
     // [A_k 36 | B_k 12 | g_k 6], which also hold block_linearize's scratch for the stage), then (once P is
     // formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values (rows of CS; CMP:
     // NN wide: the spare lanes read the next row's values, or lane CS-1's pair, and never use them)
-    constexpr int CS = (WAVES == 1) ? NN : NT;
+    constexpr int CS = (WAVES == 1 || L2W) ? NN : NT;
     constexpr int NCOLD = 11 * CS;   // 5 single rows + 3 pair rows (see the cold values below)
     constexpr int NLIN = 54 * NM;
-    constexpr int NBIG0 = (NP + NCOLD > NLIN) ? NP + NCOLD : NLIN;
+    // (L2W: the window -- X*, Y*, phi*, vref, sin / cos(phi*) -- after the stage records, read up to the condensing)
+    constexpr int NLINW = NLIN + (L2W ? 6 * (NM + 1) : 0);
+    constexpr int NBIG0 = (NP + NCOLD > NLINW) ? NP + NCOLD : NLINW;
     constexpr int NDMA = FUSED ? 0 : 2 * NT * ((27 * NM + NT - 1) / NT);   // the LDS-DMA staging tail (below)
     constexpr int NBIG = NBIG0 > NDMA ? NBIG0 : NDMA;
     __shared__ __attribute__((aligned(16))) double s_big[NBIG];
     double* const s_P = s_big;
     double* const s_cold = s_big + NP;
     __shared__ double s_xh[CLOSED ? 6 : (NM + 1) * 6];   // X_opt by the linear model (not in the closed loop)
-    __shared__ double s_sc0[CMP ? 2 : (NM + 1) * 2];
+    __shared__ double s_sc0[(CMP || L2W) ? 2 : (NM + 1) * 2];
     // exchange buffers: 4 rotating slots of NN (+ 2 more for the two-wave condensing's 2 x 3 NN), and for
     // two waves 3 fixed slots (4, 5, 6) for the ADMM loop's three exchanges, so no rotating index lives
     // across that loop (at NN = 80 it was spilled and reloaded from scratch in every exchange)
     constexpr int NEX = (WAVES > 1) ? (4 * NN + 3 * NT > 6 * NN ? 4 * NN + 3 * NT : 6 * NN) : (CMP ? 4 * NN : 6 * NN);
     constexpr int NSW = 2 * (2 * NN + 2);
     constexpr int FS = 16 * ((NN + 15) / 16);
-    constexpr int NFS = (CMP ? 1 : 2) * 4 * FS;          // condensing F_k rows: slots of 4 x FS
+    constexpr int NFS = (WAVES > 1) ? 0 : (CMP ? 1 : 2) * 4 * FS;   // condensing F_k rows: slots of 4 x FS (one wave)
     // CMP: one scratch region for the exchange / broadcast slots (ADMM, Ruiz, polish), the sweep's pivot
     // columns (factorization), the condensing's F rows and the residual transposition (8 NN + 8) -- each
     // phase leaves nothing there the next one reads.  Otherwise: exchange + sweep buffers, and s_F apart.
@@ -114,18 +135,18 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr int NSCR1 = (NFS + NWIN > 8 * NN) ? NFS + NWIN : 8 * NN;
     // CMP: the ADMM iterate (x, z, y: 5 rows of NN) is parked past the pivot columns during each K build + sweep
     constexpr int NSTASH = LEAN ? ((NSW + 1) & ~1) + 5 * NN : 0;
-    constexpr int NU0 = CMP ? ((NSCR0 > NSCR1) ? NSCR0 : NSCR1) : NEX + NSW;
+    constexpr int NU0 = CMP ? ((NSCR0 > NSCR1) ? NSCR0 : NSCR1) : (L2W ? NSCR0 : NEX + NSW);
     constexpr int NU = NU0 > NSTASH ? NU0 : NSTASH;
     __shared__ __attribute__((aligned(16))) double s_u[NU];
     double* const s_ex = s_u;                     // exchange / broadcast buffers
-    double* const s_sw = CMP ? s_u : s_u + NEX;   // sweep pivot columns (16-byte aligned: NEX is even)
-    __shared__ __attribute__((aligned(16))) double s_F0[CMP ? 2 : NFS];
+    double* const s_sw = (CMP || L2W) ? s_u : s_u + NEX;   // sweep pivot columns (16-byte aligned: NEX is even)
+    __shared__ __attribute__((aligned(16))) double s_F0[(CMP || WAVES > 1) ? 2 : NFS];
     double* const s_F = CMP ? s_u : s_F0;         // condensing: F_k rows; residual maxima
     // the reference window (X*, Y*, phi*) and vref of the stages, sin / cos(phi*_k): CMP keeps them in s_u past
     // the F slot -- read only up to the condensing (the closed loop reports no X_opt or objective)
-    double* const s_pref = CMP ? s_u + NFS : s_pref0;
-    double* const s_vref = CMP ? s_u + NFS + 3 * (NM + 1) : s_vref0;
-    double* const s_sc = CMP ? s_u + NFS + 4 * (NM + 1) : s_sc0;
+    double* const s_pref = CMP ? s_u + NFS : (L2W ? s_big + NLIN : s_pref0);
+    double* const s_vref = CMP ? s_u + NFS + 3 * (NM + 1) : (L2W ? s_big + NLIN + 3 * (NM + 1) : s_vref0);
+    double* const s_sc = CMP ? s_u + NFS + 4 * (NM + 1) : (L2W ? s_big + NLIN + 4 * (NM + 1) : s_sc0);
     __shared__ double s_red[WAVES > 1 ? 16 * WAVES : 2];
     __shared__ int s_flag[4];
 
@@ -553,9 +574,32 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 xb++;
                 if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
                 __syncthreads();
+                if constexpr (L2W) {
+                    // the three F rows in chunks of 8 entries, each chunk's reads then its FMAs (the scheduler would
+                    // otherwise issue all 240 reads beside the 160 registers of Prow); same FMAs, same order
+                    const double2* b2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(buf, 16));
 #pragma unroll
-                for (int j = 0; j < NN; ++j)
-                    Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
+                    for (int c0 = 0; c0 < NN; c0 += 8) {
+                        double2 f0[4], f1[4], f2[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            f0[i] = b2[c0 / 2 + i];
+                            f1[i] = b2[(NN + c0) / 2 + i];
+                            f2[i] = b2[(2 * NN + c0) / 2 + i];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            Prow[c0 + 2 * i] = fma(F0, f0[i].x, fma(F1, f1[i].x, fma(F2, f2[i].x, Prow[c0 + 2 * i])));
+                            Prow[c0 + 2 * i + 1] = fma(F0, f0[i].y, fma(F1, f1[i].y, fma(F2, f2[i].y, Prow[c0 + 2 * i + 1])));
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
+                    }
+                } else {
+#pragma unroll
+                    for (int j = 0; j < NN; ++j)
+                        Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
+                }
             }
         }
         __syncthreads();
@@ -682,7 +726,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             // row of P and the chunk fit the 3-wave register budget; otherwise the whole vector)
             const double* dvb = bcast(Dt);
             double c4[4] = {0.0, 0.0, 0.0, 0.0};
-            constexpr int RCH = CMP ? 8 : NN;
+            constexpr int RCH = (CMP || LEAN) ? 8 : NN;
             static_assert(NN % RCH == 0, "chunked broadcast");
 #pragma unroll
             for (int c0 = 0; c0 < NN; c0 += RCH) {
@@ -813,7 +857,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 // NN = 80: the whole vector in flight (160 VGPRs beside the 160 of Krow) spills inside the
                 // ADMM loop; CMP: the 3-wave budget (168) holds the row and a chunk.  CH values at a time
                 // (the next chunk's reads issued before this chunk's FMAs), same FMA order
-                constexpr int CH = CMP ? TGMPC_KCH : 16;
+                constexpr int CH = LEAN ? TGMPC_KCH : (CMP ? (TGMPC_KCH_W2 > 0 ? TGMPC_KCH_W2 : NN) : 16);
                 static_assert(NN % CH == 0 && CH % 2 == 0, "chunked broadcast");
                 const double2* v2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vbuf, 16));
                 double2 vb[CH / 2];
@@ -1081,7 +1125,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
                     // CMP: the pivot row in chunks of PC double2, the next chunk's reads issued before this
                     // chunk's FMAs (the whole row beside Krow does not fit the 3-wave budget)
-                    constexpr int PC = CMP ? TGMPC_PCH : NN / 2 - 1;
+                    constexpr int PC = LEAN ? TGMPC_PCH : (CMP && TGMPC_PCH_W2 > 0 ? TGMPC_PCH_W2 : NN / 2 - 1);
                     const double2 p0 = prow2[0];
                     double2 pr[PC];
 #pragma unroll
@@ -1149,6 +1193,47 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const double* prow = s_sw + o * SB + o + pv;
                     // the rotated pivot row as 20 aligned 16-byte reads, issued ahead of their FMAs
                     const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
+                    if constexpr (L2W) {
+                        // the pivot row in chunks of PC double2, the next chunk's reads issued before this chunk's
+                        // FMAs (the row of K^-1 and the whole pivot row do not fit 256 registers); same arithmetic
+                        constexpr int PC = TGMPC_PCH2;
+                        const double2 p0 = prow2[0];
+                        double2 pr[PC];
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) if (1 + i < NN / 2) pr[i] = prow2[1 + i];
+                        const double d = p0.x;
+                        ok = ok && (d > 0.0);
+                        const double dinv = rcp_nr(d);
+                        const bool piv = (t == pv);
+                        const double fd = Krow[0] * dinv;
+                        const double al = piv ? 0.0 : 1.0, be = piv ? dinv : -fd;
+                        const double k0 = piv ? -dinv : fd;
+                        const double n0 = fma(be, p0.y, al * Krow[1]);
+                        if (t < NN) {
+                            double* nb = s_sw + (o ^ 1) * SB + (o ^ 1);
+                            nb[t] = n0;
+                            nb[t + NN] = n0;
+                        }
+#pragma unroll
+                        for (int c = 1; c < NN / 2; c += PC) {
+                            double2 pn[PC];
+#pragma unroll
+                            for (int i = 0; i < PC; ++i) if (c + PC + i < NN / 2) pn[i] = prow2[c + PC + i];
+#pragma unroll
+                            for (int i = 0; i < PC; ++i) {
+                                if (c + i < NN / 2) {
+                                    const int j = 2 * (c + i);
+                                    Krow[j - 1] = fma(be, pr[i].x, al * Krow[j]);
+                                    Krow[j] = fma(be, pr[i].y, al * Krow[j + 1]);
+                                }
+                            }
+#pragma unroll
+                            for (int i = 0; i < PC; ++i) pr[i] = pn[i];
+                        }
+                        Krow[0] = n0;
+                        Krow[NN - 1] = k0;
+                        continue;
+                    }
                     double2 pr[NN / 2];
 #pragma unroll
                     for (int i = 0; i < NN / 2; ++i) pr[i] = prow2[i];
@@ -1181,6 +1266,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 }
             }
             }
+            // (L2W: the pivot columns share the exchange region -- no wave writes an exchange slot before the
+            // other has read the last pivot row)
+            if constexpr (L2W) __syncthreads();
 #pragma unroll
             for (int j = 0; j < NN; ++j) Krow[j] = -Krow[j];
             toc(cyc_sweep);

@@ -281,7 +281,7 @@ int traj_debug_fused_grid(int workgroups) {
 }
 
 int traj_debug_fused_waves(int waves) {
-    if (waves != 0 && waves != 2 && waves != 3) return TRAJ_E_ARG;
+    if (waves < 0 || waves > 3) return TRAJ_E_ARG;
     g_fused_waves = waves;
     return TRAJ_OK;
 }
@@ -590,7 +590,9 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.dbg = g_dbg;
     a.nsteps = steps;
     a.fused_grid = g_fused_grid;
-    a.wps = g_fused_waves ? g_fused_waves : (steps >= TRAJ_FUSED_W3_MIN_STEPS ? 3 : 2);
+    // kernel instance: capacity 40, 2 waves per SIMD (3 from TRAJ_FUSED_W3_MIN_STEPS steps); capacity 80, one
+    // wave per SIMD (the lean two-wave instance, traj_debug_fused_waves(2), spills at its 256 registers)
+    a.wps = g_fused_waves ? g_fused_waves : (2 * c->N > 64 ? 1 : (steps >= TRAJ_FUSED_W3_MIN_STEPS ? 3 : 2));
     a.spin_limit = g_spin_limit;
     a.dbg_items = g_dbg_items;
     carve_workspace(a, workspace, B, c->N);
