@@ -195,7 +195,7 @@ def knet_fc2_flop(B, model):
 
 
 def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
-                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r01.json"), weights=None,
+                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r03.json"), weights=None,
                  trained_json=os.path.join(HERE, "profiles", "r03_knet_trained_mse.json")):
     """Sequences/s of KalmanNet inference (BASELINE.json configs[4]) on 1024 noisy closed-loop
     trajectories x 200 steps at Ts = 0.01 generated on the GPU (knet_eval.make_sequences: the dataset
@@ -489,11 +489,11 @@ def parse_args(argv=None):
                     help="skip the one-trajectory measurement (configs[0]: drop-in per call, fused B=1, oracle 1 thread)")
     ap.add_argument("--per-step", action="store_true",
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r02.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r03.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
-    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r02.json"),
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r03.json"),
                     help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
-    ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r01.json"),
+    ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r03.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
     ap.add_argument("--knet-weights", default=None,
                     help="safetensors of trained KalmanNet weights (tools/knet_train_eval.py --save) for configs[4]")
@@ -627,7 +627,7 @@ def bench_run(args, ops, dist, rank, world):
         try:
             with open(args.issue_json) as f:
                 ij = json.load(f)
-            if ij.get("batch") == B and N == 20:
+            if ij.get("batch") == B and ij.get("horizon", 20) == N:
                 # solve_kernel is VALU-issue/latency bound: the issued f64 lane-FLOP rate against the f64
                 # vector peak, and the VALU issue slots used (4 cycles per wave64 instruction)
                 fl = ij["f64_flop_issued_per_step"] * value / world / 1e12

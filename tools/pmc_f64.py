@@ -23,6 +23,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--batch", type=int, required=True)
     ap.add_argument("--steps-per-launch", type=int, required=True)
+    ap.add_argument("--horizon", type=int, default=20)
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     per = defaultdict(lambda: defaultdict(float))
@@ -42,7 +43,7 @@ def main():
     f64_valu = 64.0 * (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"] + c["SQ_INSTS_VALU_TRANS_F64"]
                        + 2.0 * c["SQ_INSTS_VALU_FMA_F64"])
     f64_mfma = 512.0 * c["SQ_INSTS_VALU_MFMA_MOPS_F64"]
-    out = {"batch": a.batch, "steps_per_launch": a.steps_per_launch, "counters_per_launch": dict(c),
+    out = {"batch": a.batch, "horizon": a.horizon, "steps_per_launch": a.steps_per_launch, "counters_per_launch": dict(c),
            "valu_insts_per_step": c["SQ_INSTS_VALU"] / units,
            "f64_valu_insts_per_step": (c["SQ_INSTS_VALU_ADD_F64"] + c["SQ_INSTS_VALU_MUL_F64"]
                                        + c["SQ_INSTS_VALU_TRANS_F64"] + c["SQ_INSTS_VALU_FMA_F64"]) / units,
