@@ -239,9 +239,10 @@ int traj_debug_spin_limit(int polls);
  * ADMM iterations) run `steps` steps ahead of the level front (default 1 step, 100 per mille; 0 = plain
  * level order).  Results do not depend on it.  For experiments and tests. */
 int traj_debug_queue_lead(int steps, int per_mille);
-/* Fused-run kernel instance: 0 (default) = by launch length (3 waves per SIMD from 200 steps on where built,
- * capacity 40; else 2), 2 or 3 = forced (3 falls back to 2 where no 3-wave instance is built).  Results do not
- * depend on it (the two instances are bit-identical).  For experiments and tests. */
+/* Fused-run kernel instance, by waves per SIMD: 0 (default) = by capacity and launch length (capacity 40: 2, or
+ * 3 from 200 steps on; capacity 80: 1); 1, 2 or 3 = forced where built (capacity 40: 2 and 3; capacity 80: 1
+ * and the lean two-wave instance at 2; otherwise the default).  Results do not depend on it (the instances are
+ * bit-identical).  For experiments and tests. */
 int traj_debug_fused_waves(int waves);
 int traj_debug_kernel_times(double* ms, int* n_steps);
 

@@ -413,6 +413,29 @@ def test_fused_three_waves_bit_identical(gpu, N, warm, mode):
             assert _same(per[k], r[k]), (wv, k)
 
 
+def test_fused_capacity80_instances_bit_identical(gpu):
+    """Capacity 80 (N = 40, config 3): the one-wave-per-SIMD fused instance (the default) and the lean two-wave
+    instance held to 2 waves per SIMD (traj_debug_fused_waves(2): 39 KB LDS, chunked reads) equal the per-step
+    launches bit for bit, solver errors of the unstable N = 40 problems included."""
+    from trajectory_generation_amd import _lib
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B = 40, 0.05, 12, 48
+    w = make_workload(B, N, Ts, kind="mixed", seed=3)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    runs = {}
+    try:
+        for wv in (1, 2, 0):   # forced one wave per SIMD, forced lean two-wave, default
+            _lib.check(_lib.lib().traj_debug_fused_waves(wv), "traj_debug_fused_waves")
+            runs[wv] = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    finally:
+        _lib.lib().traj_debug_fused_waves(0)
+    for wv, r in runs.items():
+        for k in ("X", "U", "status", "iters"):
+            assert _same(per[k], r[k]), (wv, k)
+
+
 @pytest.mark.parametrize("lead", [(0, 0), (3, 500), (1, 999)])
 def test_fused_queue_lead_bit_identical(gpu, lead):
     """The fused run's queue order (heavy instances ahead of the level front, traj_debug_queue_lead) moves
