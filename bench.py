@@ -313,6 +313,74 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
     return out
 
 
+def knet_predict_measure(dev, B=1024, T=1200, cpu=True, cpu_B=32):
+    """test_prediction.py's sliding-window evaluation at its own sizes: T = 1200
+    steps per trajectory, H = 200, EVAL_STEP = 100, T_START_EVAL = 50 (10 windows per trajectory), on B
+    noisy closed-loop trajectories, test_prediction's architecture (in_mult 10) with seeded-init weights.
+    Timed end to end (normalization, initial states, the fused filter over all B trajectories, every
+    window's rollout and scores) and the rollout launch alone (HIP events).  The CPU leg is the oracle
+    (batched torch float32) on cpu_B trajectories; the reference itself runs the filter at batch size 1
+    per trajectory (test_prediction.py:52), slower still."""
+    from trajectory_generation_amd import knet as K
+    from trajectory_generation_amd import knet_eval as KE
+    from trajectory_generation_amd import knet_predict as KP
+    Ts = 0.01
+    train = KE.make_sequences(256, T, Ts=Ts, seed=3, id_offset=KE.TRAIN_ID_OFFSET, device=dev)
+    test = KE.make_sequences(B, T, Ts=Ts, seed=2, device=dev)
+    xm, xs, ym, ys, lim = KE.normalization(train)
+    torch.manual_seed(0)
+    sysm = K.VehicleModel(Ts, T, T, torch.zeros(6, 1))
+    sysm.Params.update(lim)
+    model = K.KalmanNetNN(dev)
+    model.NNBuild(sysm, in_mult_KNet=10, out_mult_KNet=40, hidden_dim_gru=128)
+    model.set_normalization(xm, xs, ym, ys)
+    model.eval()
+    runner = K.KNetSequenceRunner(model, B)
+    args = (model, sysm, test["y"], test["u"], test["x"], xm, xs, ym, ys)
+    KP.sliding_window_eval(*args, runner=runner)           # graph capture + warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    r = KP.sliding_window_eval(*args, runner=runner)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        KP.window_scores(sysm, r["x_est"], xm, xs, test["u"], test["x"])
+    e1.record()
+    torch.cuda.synchronize()
+    roll_ms = e0.elapsed_time(e1) / reps
+    W = r["n_windows"]
+    out = {"metric": f"sliding-window prediction eval windows/s (B={B}, T={T}, H={KP.H_PRED})",
+           "value": W / dt, "unit": "windows/s", "seconds": dt, "windows": W, "rollout_kernel_ms": roll_ms,
+           "rollout_windows_per_s": W / (roll_ms * 1e-3), "ade_mean": r["ade_mean"], "fde_mean": r["fde_mean"],
+           "config": {"workload": "test_prediction.py main() window loop: KalmanNetNN (in_mult 10) seeded-init weights, "
+                                  "noisy closed-loop MPC trajectories (knet_eval.make_sequences)", "batch": B, "T": T,
+                      "H": KP.H_PRED, "eval_step": KP.EVAL_STEP, "t_start": KP.T_START_EVAL, "Ts": Ts},
+           "note": "ADE / FDE of an untrained filter (plumbing, not quality)"}
+    if cpu:
+        import oracle.knet_oracle as KO  # test infrastructure: CPU-baseline leg only
+        w = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+        p = dict(KO.PARAMS)
+        p.update(lim)
+        threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+        torch.set_num_threads(threads)
+        y_n = ((test["y"][:cpu_B] - ym) / ys).cpu().numpy()
+        uc, xc = test["u"][:cpu_B].cpu().numpy(), test["x"][:cpu_B].cpu().numpy()
+        x0n = r["x0n"][:cpu_B].cpu().numpy()
+        t0 = time.perf_counter()
+        xe = KO.run_sequences(w, p, Ts, y_n, uc, x0n, *(a.cpu().numpy() for a in (xm, xs, ym, ys)))
+        KO.sliding_window_scores(xe, xm.cpu().numpy(), xs.cpu().numpy(), uc, xc, p, Ts, KP.H_PRED, KP.EVAL_STEP,
+                                 KP.T_START_EVAL)
+        dtc = time.perf_counter() - t0
+        wc = cpu_B * (W // B)
+        out["cpu_baseline"] = {"value": wc / dtc, "unit": "windows/s", "cores": threads, "kind": "port",
+                               "sample": f"{cpu_B} trajectories x {T} steps ({wc} windows), oracle/knet_oracle.py "
+                                         f"run_sequences + sliding_window_scores (torch CPU float32, {threads} threads)"}
+    return out
+
+
 def _spawn_workers(n, poll_s=0.2, grace_s=10.0, cmd=None):
     """bench.py --gpus N without a launcher: N worker processes (RANK / LOCAL_RANK / WORLD_SIZE, rendezvous
     on 127.0.0.1), each runs this script on its own GPU over RCCL; the parent never touches the GPU.  It polls
@@ -702,6 +770,7 @@ def bench_run(args, ops, dist, rank, world):
     if not args.no_knet and world == 1:
         out["knet"] = knet_measure(ops.dev, cpu=not args.no_cpu, traffic_json=args.knet_traffic_json,
                                    weights=args.knet_weights)
+        out["knet"]["prediction"] = knet_predict_measure(ops.dev, cpu=not args.no_cpu)
     if not args.no_config1 and world == 1:
         out["config1"] = config1_measure(ops.dev, cpu=not args.no_cpu)
     return out

@@ -12,6 +12,8 @@
  *   torch.nn.GRU cell (seq_len 1), gates r, z, n            traj_knet_gru_gates_f32
  *   kalman_net.py:169-178 KNet_step posterior update        traj_knet_update_f32
  *   kalman_net.py:145-216 whole step (throughput path)     traj_knet_front_f32 + traj_knet_fc2_f32 + traj_knet_back_f32
+ *   test_prediction.py:67-112,198-221 sliding-window        traj_knet_rollout_eval_f32
+ *     open-loop rollout + ADE / FDE
  *   (no reference counterpart) EKF baseline of config 5     traj_ekf_run_f64
  *
  * Conventions as trajmpc.h: device pointers, row-major, asynchronous on `stream`, 0 / TRAJ_E_*.
@@ -117,6 +119,24 @@ int traj_knet_back_front_f32(const traj_vehicle_params* p, const traj_knet_limit
                              const float* y_mean, const float* y_std, const float* u_mean, const float* u_std,
                              float* h_q, float* h_sigma, float* h_s, float* x_post, float* m1x_prior, float* dy,
                              float* x2, void* stream);
+
+/* Sliding-window open-loop prediction scoring (test_prediction.py:198-221 with rollout_open_loop :67-87,
+ * compute_metrics :89-103, get_error_profile :105-112), all windows of B sequences in one launch.
+ * Window w of sequence b starts at t = t0 + w * step (w < nwin; test_prediction.py iterates
+ * range(t0, T - H, step), whose length traj_knet_rollout_windows returns, -1 on bad arguments):
+ *   x      = x_est[b*e_sb + c*e_sc + t*e_st] * x_std + x_mean   (the filter's normalized estimates, e.g.
+ *            [B,6,T] with strides 6T, T, 1; x_mean = x_std = NULL: x_est is already real)
+ *   x_k+1  = clamp(x_k + Ts f(x_k, u[b, :, t + k]))  (k < H; u [B,2,T] in real units, as the filter's f)
+ *   e_k    = || x_k+1[X, Y] - x_gt[b, X:Y, t + 1 + k] ||   (x_gt [B,6,T] real)
+ *   ade[b*nwin + w] = mean_k e_k, fde[...] = e_{H-1}; err_profile [B*nwin, H] is written when not NULL;
+ *   pred [B*nwin, 6, H] receives the rolled-out states when not NULL.  x_gt = NULL: rollout only
+ *   (rollout_open_loop; pred required, ade / fde / err_profile unused).
+ * Requires t0 + (nwin - 1) * step + H <= T - 1 when scored, <= T for a bare rollout (TRAJ_E_ARG otherwise). */
+int traj_knet_rollout_windows(int T, int H, int t0, int step);
+int traj_knet_rollout_eval_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts, int B, int T,
+                               int H, int t0, int step, int nwin, const float* x_est, int e_sb, int e_sc, int e_st,
+                               const float* x_mean, const float* x_std, const float* u, const float* x_gt, float* ade,
+                               float* fde, float* err_profile, float* pred, void* stream);
 
 /* Build-defined EKF baseline for config 5 ("MSE vs reference EKF"; the reference has no EKF, SURVEY.md
  * 8(f) f2), float64, one thread per sequence, all T steps in one launch:

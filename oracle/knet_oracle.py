@@ -112,6 +112,50 @@ def angular_mse_db(x_est_real, x_true_real, phi_idx=2):
     return 10.0 * math.log10(float((d ** 2).mean()) + 1e-12)
 
 
+# ------------------------------------------------------------------ sliding-window prediction scoring
+# KalmanNet/test_prediction.py: rollout_open_loop :67-87, compute_metrics :89-103, get_error_profile
+# :105-112 and the window loop of main() :176-221, in float32 on CPU tensors.
+
+def rollout_open_loop(x0_real, u, t_start, H, p, Ts):
+    """x0_real [B,6], u [B,2,T] -> predicted states [B,6,H'] (H' = min(H, T - t_start); :67-87)."""
+    x, preds = x0_real, []
+    for k in range(H):
+        tu = t_start + k
+        if tu >= u.shape[2]:
+            break
+        x = f_step(x, u[:, :, tu], p, Ts)
+        preds.append(x)
+    return torch.stack(preds, 2) if preds else x0_real.unsqueeze(2)
+
+
+def error_profile(pred_real, gt_real):
+    """[B,6,H] x2 -> XY Euclidean error per step [B,H] (:95-98, :110-111)."""
+    diff = pred_real[:, :2, :] - gt_real[:, :2, :]
+    return torch.sqrt(torch.sum(diff ** 2, dim=1))
+
+
+def sliding_window_scores(x_est_norm, x_mean, x_std, u, x_gt, p, Ts, H, step, t0):
+    """main()'s window loop (:199-221) for B sequences at once: windows t in range(t0, T - H, step), the
+    rollout from the filter estimate x_est_norm[:, :, t] * x_std + x_mean (:202-203) scored against
+    x_gt[:, :, t+1 : t+1+H].  Returns ade [B, W], fde [B, W], profile [B, W, H] (float32)."""
+    f32 = lambda a: torch.as_tensor(a, dtype=torch.float32)   # noqa: E731
+    x_est_norm, u, x_gt = f32(x_est_norm), f32(u), f32(x_gt)
+    xm, xs = f32(x_mean).reshape(1, 6), f32(x_std).reshape(1, 6)
+    T = x_est_norm.shape[2]
+    ades, fdes, profs = [], [], []
+    for t in range(t0, T - H, step):
+        x_start = x_est_norm[:, :, t] * xs + xm
+        pred = rollout_open_loop(x_start, u, t, H, p, Ts)
+        e = error_profile(pred, x_gt[:, :, t + 1:t + 1 + H])
+        ades.append(e.mean(1))
+        fdes.append(e[:, -1])
+        profs.append(e)
+    if not ades:
+        B = x_est_norm.shape[0]
+        return torch.zeros(B, 0), torch.zeros(B, 0), torch.zeros(B, 0, H)
+    return torch.stack(ades, 1), torch.stack(fdes, 1), torch.stack(profs, 1)
+
+
 # ------------------------------------------------------------------ EKF baseline (no reference
 # counterpart: SURVEY.md 8(f) f2); the same algorithm as include/trajknet.h traj_ekf_run_f64, float64.
 def _veh_f64(x, d, de, p, Ts):

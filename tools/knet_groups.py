@@ -21,17 +21,19 @@ y = torch.randn((B, 5, T), device=dev)
 u = 0.2 * torch.randn((B, 2, T), device=dev)
 m1x0 = 0.5 * torch.randn((B, 6, 1), device=dev)
 ref = None
-for G in (1, 2, 4, 8):
+GS = [int(g) for g in os.environ.get("KG", "1,2,4,8").split(",")]
+EAGER = os.environ.get("KEAGER", "0") == "1"
+for G in GS:
     run = K.KNetSequenceRunner(model, B, groups=G)
-    out = run.run(y, u, m1x0, fused=True)
+    out = run.run(y, u, m1x0, fused=True, use_graph=not EAGER)
     torch.cuda.synchronize()
     ts = []
     for _ in range(3):
         t0 = time.perf_counter()
-        run.run(y, u, m1x0, fused=True)
+        run.run(y, u, m1x0, fused=True, use_graph=not EAGER)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     dt = min(ts)
     same = "same" if ref is None or torch.equal(out, ref) else "DIFF %.3g" % (out - ref).abs().max().item()
     ref = out if ref is None else ref
-    print(f"groups={G}: {B / dt:.0f} seq/s  {1e6 * dt / T:.1f} us/step  {same}", flush=True)
+    print(f"groups={G} eager={EAGER}: {B / dt:.0f} seq/s  {1e6 * dt / T:.1f} us/step  {same}", flush=True)

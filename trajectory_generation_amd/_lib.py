@@ -134,6 +134,10 @@ _SIGS = {
                                            C.POINTER(KnetNet), _V, C.c_int, _V, _V, C.c_int, C.c_int, _V, C.c_int,
                                            C.c_int, _V, C.c_int, C.c_int, _V, _V, _V, _V, _V, _V, _V, _V, _V, _V,
                                            _V, _V, _V, _V]),
+    "traj_knet_rollout_windows": (C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int]),
+    "traj_knet_rollout_eval_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float, C.c_int,
+                                             C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _V, C.c_int, C.c_int, C.c_int,
+                                             _V, _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_ekf_run_f64": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_double, C.c_int, C.c_int,
                                    _V, _V, _V, _V, _V, _V, _V, _V]),
     "traj_closed_loop_step": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.POINTER(Paths), C.c_int,

@@ -22,18 +22,9 @@ struct KP {   // vehicle parameters rounded to float32
     float Cm1, Cm2, Cr0, Cr2, Br, Cr, Dr, Bf, Cf, Df, m, Iz, lf, lr, maxAlpha, vx_zero;
 };
 
-// kalman_net.py:145-162 for one sequence: x_post (normalized) -> prior (normalized), m1y, dy = y - m1y
-__device__ __forceinline__ void prior_one(const KP& p, const traj_knet_limits& L, float Ts, const float* xp, float d,
-                                          float delta, const float* yv, int ystride, const float* xm,
-                                          const float* xs, const float* ym, const float* ys, const float* um,
-                                          const float* us, float* prior, float* m1y, float* dyo) {
-    float x[6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i) x[i] = __fadd_rn(__fmul_rn(xp[i], xs[i]), xm[i]);   // _denorm_x
-    if (um && us) {   // _denorm_u (only when u statistics were set)
-        d = __fadd_rn(__fmul_rn(d, us[0]), um[0]);
-        delta = __fadd_rn(__fmul_rn(delta, us[1]), um[1]);
-    }
+// VehicleModel.f (vehicle_model.py:109-134) on one real state: xn = clamp(x + Ts f_cont(x, u))
+__device__ __forceinline__ void veh_step(const KP& p, const traj_knet_limits& L, float Ts, const float* x, float d,
+                                         float delta, float* xn) {
     // pt_f_cont (vehicle_model.py:45-79)
     const float phi = clampf_(x[2], L.phi_min, L.phi_max);
     const float vx = clampf_(x[3], L.vx_min, L.vx_max);
@@ -60,9 +51,24 @@ __device__ __forceinline__ void prior_one(const KP& p, const traj_knet_limits& L
     // f: Euler step + clamp of all states (:109-134)
     const float lo[6] = {L.x_min, L.y_min, L.phi_min, L.vx_min, L.vy_min, L.omega_min};
     const float hi[6] = {L.x_max, L.y_max, L.phi_max, L.vx_max, L.vy_max, L.omega_max};
-    float xn[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) xn[i] = clampf_(__fadd_rn(x[i], __fmul_rn(Ts, xd[i])), lo[i], hi[i]);
+}
+
+// kalman_net.py:145-162 for one sequence: x_post (normalized) -> prior (normalized), m1y, dy = y - m1y
+__device__ __forceinline__ void prior_one(const KP& p, const traj_knet_limits& L, float Ts, const float* xp, float d,
+                                          float delta, const float* yv, int ystride, const float* xm,
+                                          const float* xs, const float* ym, const float* ys, const float* um,
+                                          const float* us, float* prior, float* m1y, float* dyo) {
+    float x[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = __fadd_rn(__fmul_rn(xp[i], xs[i]), xm[i]);   // _denorm_x
+    if (um && us) {   // _denorm_u (only when u statistics were set)
+        d = __fadd_rn(__fmul_rn(d, us[0]), um[0]);
+        delta = __fadd_rn(__fmul_rn(delta, us[1]), um[1]);
+    }
+    float xn[6];
+    veh_step(p, L, Ts, x, d, delta, xn);
     // renormalize; h = rows 0,1,3,4,5 (:136-153)
 #pragma unroll
     for (int i = 0; i < 6; ++i) prior[i] = __fdiv_rn(__fsub_rn(xn[i], xm[i]), xs[i]);
@@ -121,6 +127,66 @@ __global__ __launch_bounds__(256) void knet_update_kernel(int B, const float* __
 #pragma unroll
         for (int j = 0; j < 5; ++j) s = __fadd_rn(s, __fmul_rn(K[5 * i + j], e[j]));
         xo[6 * b + i] = __fadd_rn(xp[6 * b + i], __fmul_rn(gamma, s));
+    }
+}
+
+// test_prediction.py:198-221 for every (sequence b, window w) at once: the window starts at
+// t = t0 + w * step from the filter's estimate x_est[b, :, t] (normalized -> real, :202-203), runs
+// rollout_open_loop (:67-87: H clamped Euler steps of f with u[b, :, t + k]) and scores the XY error
+// against x_gt[b, :, t + 1 + k] (compute_metrics / get_error_profile, :89-112).  One thread per window;
+// the serial chain is H steps of the same physics as the filter's prior (veh_step).
+__global__ __launch_bounds__(64) void knet_rollout_kernel(KP p, traj_knet_limits L, float Ts, int B, int T, int H,
+                                                          int t0, int step, int nwin, const float* __restrict__ xe,
+                                                          int e_sb, int e_sc, int e_st,
+                                                          const float* __restrict__ xm, const float* __restrict__ xs,
+                                                          const float* __restrict__ u, const float* __restrict__ xg,
+                                                          float* __restrict__ ade, float* __restrict__ fde,
+                                                          float* __restrict__ prof, float* __restrict__ pred) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= B * nwin) return;
+    const int b = i / nwin, t = t0 + (i % nwin) * step;
+    const float* eb = xe + (size_t)b * e_sb + (size_t)t * e_st;
+    const float* ub = u + (size_t)b * 2 * T;
+    const float* gb = xg ? xg + (size_t)b * 6 * T : nullptr;
+    float x[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        const float v = eb[(size_t)c * e_sc];
+        x[c] = xm ? __fadd_rn(__fmul_rn(v, xs[c]), xm[c]) : v;   // x_start_norm * x_std + x_mean
+    }
+    double sum = 0.0;
+    float e = 0.0f;
+    // each step's inputs are loaded one step ahead: a launch holds about one wave per SIMD (B * nwin
+    // threads), so no other wave hides the load latency of the serial chain
+    float ud = ub[t], ue = ub[T + t], gx = gb ? gb[t + 1] : 0.0f, gy = gb ? gb[T + t + 1] : 0.0f;
+    for (int k = 0; k < H; ++k) {
+        const float cd = ud, ce = ue, cgx = gx, cgy = gy;
+        if (k + 1 < H) {
+            ud = ub[t + k + 1];
+            ue = ub[T + t + k + 1];
+            if (gb) {
+                gx = gb[t + k + 2];
+                gy = gb[T + t + k + 2];
+            }
+        }
+        float xn[6];
+        veh_step(p, L, Ts, x, cd, ce, xn);
+        if (gb) {
+            const float dx = __fsub_rn(xn[0], cgx), dyv = __fsub_rn(xn[1], cgy);
+            e = __fsqrt_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dyv, dyv)));   // sqrt(sum(diff**2)) over X, Y
+            sum += (double)e;
+            if (prof) prof[(size_t)i * H + k] = e;
+        }
+        if (pred) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) pred[((size_t)i * 6 + c) * H + k] = xn[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 6; ++c) x[c] = xn[c];
+    }
+    if (gb) {
+        ade[i] = (float)(sum / (double)H);   // err_dist.mean()
+        fde[i] = e;                          // err_dist[0, -1]
     }
 }
 
@@ -981,6 +1047,34 @@ int traj_knet_update_f32(int B, const float* x_prior, const float* KG, const flo
     if (!x_prior || !KG || !dy || !innov_logit || !x_post) return TRAJ_E_ARG;
     hipLaunchKernelGGL(knet_update_kernel, dim3(nblk(B, 256)), dim3(256), 0, (hipStream_t)stream, B, x_prior, KG, dy,
                        innov_logit, x_post);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_knet_rollout_windows(int T, int H, int t0, int step) {
+    if (T < 0 || H < 1 || t0 < 0 || step < 1) return -1;
+    const int end = T - H;   // range(t0, T - H, step)
+    return end > t0 ? (end - t0 + step - 1) / step : 0;
+}
+
+int traj_knet_rollout_eval_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts, int B, int T,
+                               int H, int t0, int step, int nwin, const float* x_est, int e_sb, int e_sc, int e_st,
+                               const float* x_mean, const float* x_std, const float* u, const float* x_gt, float* ade,
+                               float* fde, float* err_profile, float* pred, void* stream) {
+    if (!p || !lim || B < 0 || T < 0 || H < 1 || t0 < 0 || step < 1 || nwin < 0) return TRAJ_E_ARG;
+    // every window's inputs u[:, :, t .. t + H - 1] (and, when scored, its ground truth x_gt[:, :, t + 1 .. t + H])
+    // lie inside the sequence
+    if (nwin > 0 && (long long)t0 + (long long)(nwin - 1) * step + H > (long long)T - (x_gt ? 1 : 0))
+        return TRAJ_E_ARG;
+    if ((long long)B * nwin > 0x7fffffffLL || e_sb < 0 || e_sc < 0 || e_st < 0) return TRAJ_E_ARG;
+    if (B == 0 || nwin == 0) return TRAJ_OK;
+    if (!x_est || !u || (!x_mean) != (!x_std)) return TRAJ_E_ARG;
+    if (x_gt ? (!ade || !fde) : !pred) return TRAJ_E_ARG;
+    KP k{(float)p->Cm1, (float)p->Cm2, (float)p->Cr0, (float)p->Cr2, (float)p->Br, (float)p->Cr, (float)p->Dr,
+         (float)p->Bf,  (float)p->Cf,  (float)p->Df,  (float)p->m,   (float)p->Iz, (float)p->lf, (float)p->lr,
+         (float)p->maxAlpha, (float)p->vx_zero};
+    hipLaunchKernelGGL(knet_rollout_kernel, dim3(nblk((long long)B * nwin, 64)), dim3(64), 0, (hipStream_t)stream, k,
+                       *lim, Ts, B, T, H, t0, step, nwin, x_est, e_sb, e_sc, e_st, x_mean, x_std, u, x_gt, ade, fde,
+                       x_gt ? err_profile : nullptr, pred);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
