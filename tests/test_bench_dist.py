@@ -1,4 +1,4 @@
-"""bench.py's multi-rank path on CPU (no GPU): bench_run's distributed branch end to end at world size 2
+"""bench.py's multi-rank path on CPU (no GPU): bench_run's distributed branch end to end at world sizes 2 and 4
 over gloo -- barriers, the MAX all-reduce of the elapsed time, the dataset leg's gather into rank 0, the
 record on rank 0 only -- with a CPU stand-in for the device side; and the launcher's failure handling (a
 worker that dies takes its siblings down, the parent exits with its status)."""
@@ -65,42 +65,44 @@ def _free_port():
     return p
 
 
-def _rank(rank, port, q, csv_dir):
-    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1",
+def _rank(rank, port, q, csv_dir, world=2):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import bench
-    out = bench.main(["--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "4", "--dataset-steps", "5",
+    out = bench.main(["--gpus", str(world), "--steps", "3", "--warmup", "1", "--batch", "4", "--dataset-steps", "5",
                       "--no-cpu", "--no-knet", "--dist-timeout", "120", "--dataset-csv", csv_dir],
                      ops_factory=CpuOps, backend="gloo")
     q.put((rank, out))
 
 
-def test_bench_run_two_ranks_gloo(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_run_multi_rank_gloo(tmp_path, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, port, q, str(tmp_path))) for r in range(2)]
+    procs = [ctx.Process(target=_rank, args=(r, port, q, str(tmp_path), world)) for r in range(world)]
     for p in procs:
         p.start()
-    got = dict(q.get(timeout=180) for _ in range(2))
+    got = dict(q.get(timeout=180) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got[1] is None                                   # one record, from rank 0
+    assert all(got[r] is None for r in range(1, world))     # one record, from rank 0
     out = got[0]
-    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 8 and out["scaling"] == "weak"
-    assert out["value"] == pytest.approx(8 * 3 / (out["ms_per_step"] * 3 / 1e3))   # whole-job steps / max elapsed
+    G = 4 * world
+    assert out["n_gpus"] == world and out["config"]["global_batch"] == G and out["scaling"] == "weak"
+    assert out["value"] == pytest.approx(G * 3 / (out["ms_per_step"] * 3 / 1e3))   # whole-job steps / max elapsed
     assert out["ms_per_step"] >= 18.0                       # the MAX over ranks: rank 1's 60 ms for 3 steps
     assert out["cold"]["iters_mean"] == 50.0 and out["solver_stats"]["iters_mean"] == 25.0
     ds = out["dataset"]
-    assert ds["trajectories"] == 8 and ds["steps"] == 5 and ds["gather_bytes"] == 8 * 6 * 9 * 8
-    assert ds["status_hist"][0] == 8 * 5 and ds["failed_trajectories"] == 0
-    # the gathered files on rank 0 and one shard per rank (ids 0-3, 4-7), each with its status sidecar
+    assert ds["trajectories"] == G and ds["steps"] == 5 and ds["gather_bytes"] == G * 6 * 9 * 8
+    assert ds["status_hist"][0] == G * 5 and ds["failed_trajectories"] == 0
+    # the gathered files on rank 0 and one shard per rank (ids 4r .. 4r+3), each with its status sidecar
     assert ds["csv_s"] is not None and ds["csv_shards_s"] is not None
     one = open(tmp_path / "vehicle_mpc_clean.csv").read().splitlines()
-    sh = [open(tmp_path / f"vehicle_mpc_rank{r}_clean.csv").read().splitlines() for r in range(2)]
-    assert sh[0][1:] + sh[1][1:] == one[1:] and len(one) == 1 + 8 * 6
-    for r in range(2):
+    sh = [open(tmp_path / f"vehicle_mpc_rank{r}_clean.csv").read().splitlines() for r in range(world)]
+    assert sum((x[1:] for x in sh), []) == one[1:] and len(one) == 1 + G * 6
+    for r in range(world):
         assert len(open(tmp_path / f"vehicle_mpc_rank{r}_status.csv").read().splitlines()) == 5
 
 

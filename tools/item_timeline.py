@@ -126,4 +126,6 @@ def main(steps=20, warm=5, B=4096, N=20, Ts=0.05, kind="spline", out=None, lead=
 
 if __name__ == "__main__":
     a = [int(v) for v in sys.argv[1:4]]
-    main(*a)
+    # TL_N / TL_KIND: horizon and reference kind (config 3: TL_N=40 TL_KIND=mixed)
+    main(*a, N=int(os.environ.get("TL_N", 20)), kind=os.environ.get("TL_KIND", "spline"),
+         out=os.environ.get("TL_OUT"))
