@@ -40,6 +40,9 @@
 #endif
 #ifndef TGMPC_PCH
 #define TGMPC_PCH 4            // CMP: pivot-row double2 per chunk of the sweep
+#ifndef TGMPC_NSTASH
+#define TGMPC_NSTASH 3         // 3-wave instance: ADMM iterate rows parked in LDS across the factorization (of 5)
+#endif
 #endif
 #ifndef TGMPC_L2W_WPE
 #define TGMPC_L2W_WPE 2        // waves per SIMD the lean two-wave instance is built for
@@ -134,7 +137,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr int NWIN = CMP ? 6 * (NM + 1) : 0;   // CMP: the window and sin/cos(phi*) after the F slot
     constexpr int NSCR1 = (NFS + NWIN > 8 * NN) ? NFS + NWIN : 8 * NN;
     // CMP: the ADMM iterate (x, z, y: 5 rows of NN) is parked past the pivot columns during each K build + sweep
-    constexpr int NSTASH = LEAN ? ((NSW + 1) & ~1) + 5 * NN : 0;
+    // (the 3-wave instance parks TGMPC_NSTASH of the 5 rows: with 3 the LDS image is <= 12,800 B, so 12 workgroups
+    // fit a CU's 160 KB at gfx950's 1,280-byte allocation granule instead of 11)
+    constexpr int NSTR = (CMP && LEAN) ? TGMPC_NSTASH : 5;
+    constexpr int NSTASH = LEAN ? ((NSW + 1) & ~1) + NSTR * NN : 0;
     constexpr int NU0 = CMP ? ((NSCR0 > NSCR1) ? NSCR0 : NSCR1) : (L2W ? NSCR0 : NEX + NSW);
     constexpr int NU = NU0 > NSTASH ? NU0 : NSTASH;
     __shared__ __attribute__((aligned(16))) double s_u[NU];
@@ -1019,18 +1025,26 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         auto tic = [&]() { if (prof) t_mark = __builtin_amdgcn_s_memtime(); };
         auto toc = [&](long long& acc) { if (prof) acc += __builtin_amdgcn_s_memtime() - t_mark; };
         // LEAN: the iterate is parked in LDS (past the sweep's pivot columns) from before the K build to after the
-        // sweep -- the factorization is the kernel's register peak, and values live across it are spilled
+        // sweep -- the factorization is the kernel's register peak, and values live across it are spilled.  The
+        // 3-wave instance parks z and y_b (NSTR = 3) and keeps x, y_r in registers: its scratch stays at 256 B
+        // and the LDS image at 12,776 B (12 workgroups per CU; all five rows: 13,128 B, 11)
         typedef __attribute__((address_space(3))) volatile double* LdsVDs;
         auto stash = [&]() {
             if constexpr (LEAN) {
                 LdsVDs sp = (LdsVDs)(s_u + ((NSW + 1) & ~1));
-                if (t < NN) { sp[t] = x; sp[NN + t] = zb; sp[2 * NN + t] = zr; sp[3 * NN + t] = yb; sp[4 * NN + t] = yr; }
+                if (t < NN) {
+                    sp[t] = zb; sp[NN + t] = zr; sp[2 * NN + t] = yb;
+                    if (NSTR > 3) sp[3 * NN + t] = yr;
+                    if (NSTR > 4) sp[4 * NN + t] = x;
+                }
             }
         };
         auto unstash = [&]() {
             if constexpr (LEAN) {
                 LdsVDs sp = (LdsVDs)(s_u + ((NSW + 1) & ~1));
-                x = sp[tc]; zb = sp[NN + tc]; zr = sp[2 * NN + tc]; yb = sp[3 * NN + tc]; yr = sp[4 * NN + tc];
+                zb = sp[tc]; zr = sp[NN + tc]; yb = sp[2 * NN + tc];
+                if (NSTR > 3) yr = sp[3 * NN + tc];
+                if (NSTR > 4) x = sp[4 * NN + tc];
             }
         };
         while (phase != PH_DONE) {
