@@ -53,6 +53,12 @@
 #ifndef TGMPC_PCH_W2
 #define TGMPC_PCH_W2 4         // fused one-wave instance at 2 waves per SIMD: pivot-row double2 per chunk (0: all)
 #endif
+#ifndef TGMPC_KCH80
+#define TGMPC_KCH80 16         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec
+#endif
+#ifndef TGMPC_PCH80
+#define TGMPC_PCH80 4          // capacity 80, one wave per SIMD: pivot-row double2 per chunk of the sweep (0: whole row)
+#endif
 #ifndef TGMPC_PCH2
 #define TGMPC_PCH2 4           // L2W: pivot-row double2 per chunk of the two-wave sweep
 #endif
@@ -863,7 +869,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 // NN = 80: the whole vector in flight (160 VGPRs beside the 160 of Krow) spills inside the
                 // ADMM loop; CMP: the 3-wave budget (168) holds the row and a chunk.  CH values at a time
                 // (the next chunk's reads issued before this chunk's FMAs), same FMA order
-                constexpr int CH = LEAN ? TGMPC_KCH : (CMP ? (TGMPC_KCH_W2 > 0 ? TGMPC_KCH_W2 : NN) : 16);
+                constexpr int CH = LEAN ? TGMPC_KCH : (CMP ? (TGMPC_KCH_W2 > 0 ? TGMPC_KCH_W2 : NN) : TGMPC_KCH80);
                 static_assert(NN % CH == 0 && CH % 2 == 0, "chunked broadcast");
                 const double2* v2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vbuf, 16));
                 double2 vb[CH / 2];
@@ -1207,10 +1213,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const double* prow = s_sw + o * SB + o + pv;
                     // the rotated pivot row as 20 aligned 16-byte reads, issued ahead of their FMAs
                     const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
-                    if constexpr (L2W) {
+                    if constexpr (L2W || (WAVES > 1 && TGMPC_PCH80 > 0)) {
                         // the pivot row in chunks of PC double2, the next chunk's reads issued before this chunk's
                         // FMAs (the row of K^-1 and the whole pivot row do not fit 256 registers); same arithmetic
-                        constexpr int PC = TGMPC_PCH2;
+                        constexpr int PC = L2W ? TGMPC_PCH2 : (TGMPC_PCH80 > 0 ? TGMPC_PCH80 : 1);
                         const double2 p0 = prow2[0];
                         double2 pr[PC];
 #pragma unroll
