@@ -431,6 +431,9 @@ class GpuOps:
         torch.cuda.set_device(self.dev)
         if os.environ.get("TRAJ_FUSED_WAVES"):   # experiments: force the fused kernel instance (traj_debug_fused_waves)
             _lib.check(_lib.lib().traj_debug_fused_waves(int(os.environ["TRAJ_FUSED_WAVES"])), "traj_debug_fused_waves")
+        if os.environ.get("TRAJ_QUEUE_LEAD"):    # experiments: "steps,per_mille" of the fused queue's lead set
+            ls, lp = (int(v) for v in os.environ["TRAJ_QUEUE_LEAD"].split(","))
+            _lib.check(_lib.lib().traj_debug_queue_lead(ls, lp), "traj_debug_queue_lead")
 
     def sync(self):
         torch.cuda.synchronize()
