@@ -53,6 +53,12 @@
 #ifndef TGMPC_PCH_W2
 #define TGMPC_PCH_W2 4         // fused one-wave instance at 2 waves per SIMD: pivot-row double2 per chunk (0: all)
 #endif
+#ifndef TGMPC_RCH80
+#define TGMPC_RCH80 1          // capacity 80, one wave per SIMD: Ruiz reads the broadcast D in chunks of 8
+#endif
+#ifndef TGMPC_PMUL80
+#define TGMPC_PMUL80 1         // capacity 80, one wave per SIMD: the rolled P v of the 3-wave instance
+#endif
 #ifndef TGMPC_KCH80
 #define TGMPC_KCH80 16         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec
 #endif
@@ -738,7 +744,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             // row of P and the chunk fit the 3-wave register budget; otherwise the whole vector)
             const double* dvb = bcast(Dt);
             double c4[4] = {0.0, 0.0, 0.0, 0.0};
-            constexpr int RCH = (CMP || LEAN) ? 8 : NN;
+            constexpr int RCH = (CMP || LEAN || (WAVES > 1 && TGMPC_RCH80)) ? 8 : NN;
             static_assert(NN % RCH == 0, "chunked broadcast");
 #pragma unroll
             for (int c0 = 0; c0 < NN; c0 += RCH) {
@@ -839,7 +845,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double* vb = bcast(v);
             const int tt = opaque_t();
             double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-            if constexpr (LEAN) {
+            if constexpr (LEAN || (WAVES > 1 && TGMPC_PMUL80)) {
                 // a ROLLED loop over blocks of 8 (the row of K^-1 stays live across this: fully unrolled, the
                 // scheduler issues all 80 reads at once and the ADMM loop around it spills); same sums, same order
                 static_assert(NN % 8 == 0, "Pmul blocks");
