@@ -59,6 +59,9 @@
 #ifndef TGMPC_PMUL80
 #define TGMPC_PMUL80 1         // capacity 80, one wave per SIMD: the rolled P v of the 3-wave instance
 #endif
+#ifndef TGMPC_PMUL_W2
+#define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
+#endif
 #ifndef TGMPC_KCH80
 #define TGMPC_KCH80 16         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec
 #endif
@@ -845,7 +848,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double* vb = bcast(v);
             const int tt = opaque_t();
             double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-            if constexpr (LEAN || (WAVES > 1 && TGMPC_PMUL80)) {
+            if constexpr (LEAN || (WAVES > 1 && TGMPC_PMUL80) || (CMP && TGMPC_PMUL_W2)) {
                 // a ROLLED loop over blocks of 8 (the row of K^-1 stays live across this: fully unrolled, the
                 // scheduler issues all 80 reads at once and the ADMM loop around it spills); same sums, same order
                 static_assert(NN % 8 == 0, "Pmul blocks");
