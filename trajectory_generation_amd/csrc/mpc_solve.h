@@ -59,6 +59,9 @@
 #ifndef TGMPC_PMUL80
 #define TGMPC_PMUL80 1         // capacity 80, one wave per SIMD: the rolled P v of the 3-wave instance
 #endif
+#ifndef TGMPC_COND80
+#define TGMPC_COND80 0         // capacity 80, one wave per SIMD: the condensing reads the F rows in chunks of 8
+#endif
 #ifndef TGMPC_PMUL_W2
 #define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
 #endif
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 xb++;
                 if (own) { buf[t] = F0; buf[NN + t] = F1; buf[2 * NN + t] = F2; }
                 __syncthreads();
-                if constexpr (L2W) {
+                if constexpr (L2W || TGMPC_COND80) {
                     // the three F rows in chunks of 8 entries, each chunk's reads then its FMAs (the scheduler would
                     // otherwise issue all 240 reads beside the 160 registers of Prow); same FMAs, same order
                     const double2* b2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(buf, 16));
