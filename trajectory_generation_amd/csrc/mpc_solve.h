@@ -59,6 +59,14 @@
 #ifndef TGMPC_PMUL80
 #define TGMPC_PMUL80 1         // capacity 80, one wave per SIMD: the rolled P v of the 3-wave instance
 #endif
+#ifndef TGMPC_SWEEP_UNROLL
+#define TGMPC_SWEEP_UNROLL 4   // one-wave sweep: pivots per unrolled loop body (1: rolled, NN register moves per pivot)
+#endif
+#ifndef TGMPC_SWEEP_UNROLL2
+#define TGMPC_SWEEP_UNROLL2 1  // two-wave sweep (capacity 80): the same
+#endif
+#define TGMPC_PRAGMA_(x) _Pragma(#x)
+#define TGMPC_PRAGMA(x) TGMPC_PRAGMA_(x)
 #ifndef TGMPC_COND80
 #define TGMPC_COND80 0         // capacity 80, one wave per SIMD: the condensing reads the F rows in chunks of 8
 #endif
@@ -1142,7 +1150,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     s_sw[t] = Krow[0];
                     s_sw[t + NN] = Krow[0];
                 }
-#pragma nounroll
+                // unrolled by TGMPC_SWEEP_UNROLL: the register rotation is static inside the unrolled body, so
+                // realigning the row costs NN register moves per TGMPC_SWEEP_UNROLL pivots instead of per pivot
+                TGMPC_PRAGMA(unroll TGMPC_SWEEP_UNROLL)
                 for (int pv = 0; pv < NN; ++pv) {
                     if (NN > SPARE && pv == SPARE) {
                         // lanes 0..SPARE-1 all pivoted (dropped rows): zero them, they receive next
@@ -1218,7 +1228,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     s_sw[t] = Krow[0];
                     s_sw[t + NN] = Krow[0];
                 }
-#pragma nounroll
+                TGMPC_PRAGMA(unroll TGMPC_SWEEP_UNROLL2)
                 for (int pv = 0; pv < NN; ++pv) {
                     __syncthreads();
                     const int o = pv & 1;
