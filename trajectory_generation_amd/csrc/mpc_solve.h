@@ -63,10 +63,13 @@
 #define TGMPC_SWEEP_UNROLL 4   // one-wave sweep: pivots per unrolled loop body (1: rolled, NN register moves per pivot)
 #endif
 #ifndef TGMPC_SWEEP_UNROLL2
-#define TGMPC_SWEEP_UNROLL2 1  // two-wave sweep (capacity 80): the same
+#define TGMPC_SWEEP_UNROLL2 4  // two-wave sweep (capacity 80): the same
 #endif
 #define TGMPC_PRAGMA_(x) _Pragma(#x)
 #define TGMPC_PRAGMA(x) TGMPC_PRAGMA_(x)
+#ifndef TGMPC_RECV2
+#define TGMPC_RECV2 1          // capacity 80, one wave per SIMD: the receiver-lane sweep (one fma per entry and pivot)
+#endif
 #ifndef TGMPC_COND80
 #define TGMPC_COND80 0         // capacity 80, one wave per SIMD: the condensing reads the F rows in chunks of 8
 #endif
@@ -137,6 +140,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values (rows of CS; CMP:
     // NN wide: the spare lanes read the next row's values, or lane CS-1's pair, and never use them)
     constexpr int CS = (WAVES == 1 || L2W) ? NN : NT;
+    // the two-wave receiver sweep (capacity 80 at one wave per SIMD): rows start shifted by SP2 lanes
+    constexpr bool RECV2 = WAVES == 2 && !L2W && TGMPC_RECV2;
+    constexpr int SP2 = 64 * WAVES - NN;
     constexpr int NCOLD = 11 * CS;   // 5 single rows + 3 pair rows (see the cold values below)
     constexpr int NLIN = 54 * NM;
     // (L2W: the window -- X*, Y*, phi*, vref, sin / cos(phi*) -- after the stage records, read up to the condensing)
@@ -1106,7 +1112,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     }
                 }
                 __syncthreads();
-                if (WAVES > 1 || t < NN) {
+                if constexpr (RECV2) {
+                    // two-wave receiver sweep: lane t holds row t - SP2 (lanes < SP2: exact zero rows)
+                    const int r = tt - SP2;
+                    const int rr = r >= 0 ? r : 0;
+#pragma unroll
+                    for (int j = 0; j < NN; ++j) Krow[j] = (r >= 0) ? s_P[paddr(j, rr)] : 0.0;
+                } else if (WAVES > 1 || t < NN) {
 #pragma unroll
                     for (int j = 0; j < NN; ++j) Krow[j] = (WAVES == 1 || t < NN) ? s_P[paddr(j, tt)] : 0.0;
                 } else {
@@ -1215,6 +1227,70 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(Krow[j]));
                     Krow[j] = __hiloint2double(hi, lo);
                     __builtin_amdgcn_sched_barrier(0);   // one register at a time (no batch of 80 temporaries)
+                }
+            } else if constexpr (RECV2) {
+                // Two-wave sweep (capacity 80, one wave per SIMD), ONE fma per entry and pivot: the receiver
+                // form of the one-wave sweep above.  Rows start SHIFTED: lane t holds row t - SP2 (SP2 = 128 - NN
+                // spare lanes first, holding exact zero rows).  Pivot pv's new row K_pj / d is formed in
+                // receiver lane pv -- a spare lane while pv < SP2; the lanes SP2..NN-1 held rows 0..NN-SP2-1,
+                // all dropped by pivot NN - SP2 and zeroed then -- so row r ends in lane r: no final
+                // permutation across the waves.  Same values as the two-operation form (see above).
+                constexpr int SB = 2 * NN + 2;
+                static_assert(NN <= 2 * SP2, "receivers: the spare lanes, then the first dropped rows' lanes");
+                int rho = (t >= SP2) ? t - SP2 : -1;   // row held by this lane (-1: zero or dropped)
+                if (rho >= 0) {
+                    s_sw[rho] = Krow[0];
+                    s_sw[rho + NN] = Krow[0];
+                }
+                TGMPC_PRAGMA(unroll TGMPC_SWEEP_UNROLL2)
+                for (int pv = 0; pv < NN; ++pv) {
+                    if (NN > SP2 && pv == NN - SP2) {
+                        if (t >= SP2 && t < NN) {
+#pragma unroll
+                            for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
+                        }
+                    }
+                    __syncthreads();
+                    const int o = pv & 1;
+                    const double* prow = s_sw + o * SB + o + pv;
+                    const double2* prow2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(prow, 16));
+                    constexpr int PC = TGMPC_PCH80 > 0 ? TGMPC_PCH80 : 1;
+                    const double2 p0 = prow2[0];
+                    double2 pr[PC];
+#pragma unroll
+                    for (int i = 0; i < PC; ++i) if (1 + i < NN / 2) pr[i] = prow2[1 + i];
+                    const double d = p0.x;
+                    ok = ok && (d > 0.0);
+                    const double dinv = rcp_nr(d);
+                    const bool recv = (t == pv);
+                    const double fd = Krow[0] * dinv;
+                    const double be = recv ? dinv : -fd;
+                    const double k0 = recv ? -dinv : fd;
+                    rho = recv ? pv : ((t == SP2 + pv) ? -1 : rho);
+                    const double n0 = fma3(be, p0.y, Krow[1]);
+                    if (rho >= 0) {
+                        double* nb = s_sw + (o ^ 1) * SB + (o ^ 1);
+                        nb[rho] = n0;
+                        nb[rho + NN] = n0;
+                    }
+#pragma unroll
+                    for (int c = 1; c < NN / 2; c += PC) {
+                        double2 pn[PC];
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) if (c + PC + i < NN / 2) pn[i] = prow2[c + PC + i];
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) {
+                            if (c + i < NN / 2) {
+                                const int j = 2 * (c + i);
+                                Krow[j - 1] = fma3(be, pr[i].x, Krow[j]);
+                                Krow[j] = fma3(be, pr[i].y, Krow[j + 1]);
+                            }
+                        }
+#pragma unroll
+                        for (int i = 0; i < PC; ++i) pr[i] = pn[i];
+                    }
+                    Krow[0] = n0;
+                    Krow[NN - 1] = k0;
                 }
             } else {
             {
