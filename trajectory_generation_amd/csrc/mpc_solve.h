@@ -85,6 +85,9 @@
 #ifndef TGMPC_PCH2
 #define TGMPC_PCH2 4           // L2W: pivot-row double2 per chunk of the two-wave sweep
 #endif
+#ifndef TGMPC_RECV2_L2W
+#define TGMPC_RECV2_L2W 1      // L2W: the receiver sweep as well (scratch 1,864 -> 396 B/lane; still opt-in)
+#endif
 
 namespace tgmpc {
 
@@ -140,8 +143,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // formed) the scaled P as a packed upper triangle (row-major) + per-lane cold values (rows of CS; CMP:
     // NN wide: the spare lanes read the next row's values, or lane CS-1's pair, and never use them)
     constexpr int CS = (WAVES == 1 || L2W) ? NN : NT;
-    // the two-wave receiver sweep (capacity 80 at one wave per SIMD): rows start shifted by SP2 lanes
-    constexpr bool RECV2 = WAVES == 2 && !L2W && TGMPC_RECV2;
+    // the two-wave receiver sweep (capacity 80; the lean two-wave instance too): rows start shifted by SP2 lanes
+    constexpr bool RECV2 = WAVES == 2 && (!L2W || TGMPC_RECV2_L2W) && TGMPC_RECV2;
     constexpr int SP2 = 64 * WAVES - NN;
     constexpr int NCOLD = 11 * CS;   // 5 single rows + 3 pair rows (see the cold values below)
     constexpr int NLIN = 54 * NM;
