@@ -7,6 +7,10 @@ vehicle_model.VehicleModel / pt_f_cont / pt_tire_forces (:1-153).  Weights are t
 set of tests/_knet_weights.py (loaded with load_state_dict), eval mode (dropout off), float32 as the
 reference runs.  Inputs are synthetic: B=4 sequences of T=20 steps simulated with the reference's own
 VehicleModel.f from random initial states and random controls, observed through h with noise.
+
+A second set, knet_b37_t60_im10.npz, covers a ragged batch (B=37, not a multiple of the 4 sequences a fused
+workgroup owns), a longer recurrence (T=60) and the in_mult 10 architecture (training.py / test_prediction.py,
+FC5 60 wide) with weight seed 2.
 """
 import os
 import sys
@@ -22,13 +26,13 @@ from tests._knet_weights import LIMITS, knet_weights  # noqa: E402
 REF = "/root/reference/KalmanNet"
 
 
-def main():
+def main(B=4, T=20, in_mult=5, wseed=0, rseed=7, fname="knet.npz"):
     sys.path.insert(0, REF)
     import kalman_net as KN
     import vehicle_model as VM
     torch.set_num_threads(4)
-    Ts, B, T = 0.01, 4, 20
-    rng = np.random.default_rng(7)
+    Ts = 0.01
+    rng = np.random.default_rng(rseed)
     params = dict(VM.Params)
     params.update(LIMITS)
     sysm = VM.VehicleModel(Ts, T, T, torch.zeros(6, 1), None, None, None)
@@ -64,9 +68,9 @@ def main():
     f32 = lambda a: torch.tensor(a, dtype=torch.float32)   # noqa: E731
 
     model = KN.KalmanNetNN()
-    model.NNBuild(sysm, in_mult_KNet=5, out_mult_KNet=40, hidden_dim_gru=128)
+    model.NNBuild(sysm, in_mult_KNet=in_mult, out_mult_KNet=40, hidden_dim_gru=128)
     model.set_normalization(f32(x_mean), f32(x_std), f32(y_mean), f32(y_std))
-    sd = {k: torch.tensor(v) for k, v in knet_weights(seed=0).items()}
+    sd = {k: torch.tensor(v) for k, v in knet_weights(seed=wseed, in_mult=in_mult).items()}
     model.load_state_dict(sd)
     model.eval()
     y_norm = (Y - y_mean) / y_std
@@ -82,13 +86,16 @@ def main():
             prior.append(model.m1x_prior.squeeze(2).numpy())
             kg.append(model.KGain.numpy())
     np.savez_compressed(
-        os.path.join(HERE, "knet.npz"), Ts=Ts, seed=0, in_mult=5, out_mult=40, hidden=128,
+        os.path.join(HERE, fname), Ts=Ts, seed=wseed, in_mult=in_mult, out_mult=40, hidden=128,
         limits=np.array([LIMITS[k] for k in sorted(LIMITS)]), limit_names=np.array(sorted(LIMITS)),
         phys_x=xp, phys_u=up, pt_f_cont=f_cont, f_step=f_step,
         x_mean=x_mean, x_std=x_std, y_mean=y_mean, y_std=y_std, y_norm=y_norm, u=U, x_true=X, m1x0=m1x0,
         x_post=np.stack(post, 2), x_prior=np.stack(prior, 2), KG=np.stack(kg, 3))
-    print("wrote knet.npz", np.stack(post, 2).shape)
+    print("wrote", fname, np.stack(post, 2).shape)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "b37":
+        main(B=37, T=60, in_mult=10, wseed=2, rseed=23, fname="knet_b37_t60_im10.npz")
+    else:
+        main()

@@ -12,14 +12,14 @@ pytestmark = pytest.mark.gpu
 G = np.load("tests/golden/knet.npz")
 
 
-def build(dev, seed=0, in_mult=5):
+def build(dev, seed=0, in_mult=5, g=G):
     from trajectory_generation_amd import knet as K
-    sysm = K.VehicleModel(float(G["Ts"]), 20, 20, torch.zeros(6, 1))
+    sysm = K.VehicleModel(float(g["Ts"]), 20, 20, torch.zeros(6, 1))
     sysm.Params.update(LIMITS)
     model = K.KalmanNetNN(dev)
     model.NNBuild(sysm, in_mult_KNet=in_mult, out_mult_KNet=40, hidden_dim_gru=128)
     f32 = lambda a: torch.tensor(a, dtype=torch.float32)   # noqa: E731
-    model.set_normalization(f32(G["x_mean"]), f32(G["x_std"]), f32(G["y_mean"]), f32(G["y_std"]))
+    model.set_normalization(f32(g["x_mean"]), f32(g["x_std"]), f32(g["y_mean"]), f32(g["y_std"]))
     sd = {k: torch.tensor(v) for k, v in knet_weights(seed=seed, in_mult=in_mult).items()}
     model.load_state_dict(sd, strict=True)
     model.eval()
@@ -49,12 +49,14 @@ def test_missing_limits_raise_like_reference(gpu):
         sysm.f(x, u)
 
 
-def test_sequence_vs_reference(gpu):
-    _, _, model = build(gpu)
-    B, T = G["y_norm"].shape[0], G["y_norm"].shape[2]
-    y = torch.tensor(G["y_norm"], dtype=torch.float32, device=gpu)
-    u = torch.tensor(G["u"], dtype=torch.float32, device=gpu)
-    m1x0 = torch.tensor(G["m1x0"], dtype=torch.float32, device=gpu)
+@pytest.mark.parametrize("name", ["knet.npz", "knet_b37_t60_im10.npz"])
+def test_sequence_vs_reference(gpu, name):
+    g = np.load("tests/golden/" + name)
+    _, _, model = build(gpu, seed=int(g["seed"]), in_mult=int(g["in_mult"]), g=g)
+    B, T = g["y_norm"].shape[0], g["y_norm"].shape[2]
+    y = torch.tensor(g["y_norm"], dtype=torch.float32, device=gpu)
+    u = torch.tensor(g["u"], dtype=torch.float32, device=gpu)
+    m1x0 = torch.tensor(g["m1x0"], dtype=torch.float32, device=gpu)
     with torch.no_grad():
         model.batch_size = B
         model.init_hidden_KNet()
@@ -65,9 +67,9 @@ def test_sequence_vs_reference(gpu):
             priors.append(model.m1x_prior.squeeze(2).cpu().numpy())
             kgs.append(model.KGain.cpu().numpy())
     post, prior, kg = np.stack(posts, 2), np.stack(priors, 2), np.stack(kgs, 3)
-    assert np.abs(prior - G["x_prior"]).max() <= tol(G["x_prior"])
-    assert np.abs(kg - G["KG"]).max() <= tol(G["KG"])
-    assert np.abs(post - G["x_post"]).max() <= tol(G["x_post"])
+    assert np.abs(prior - g["x_prior"]).max() <= tol(g["x_prior"])
+    assert np.abs(kg - g["KG"]).max() <= tol(g["KG"])
+    assert np.abs(post - g["x_post"]).max() <= tol(g["x_post"])
     # reference attribute shapes
     assert model.m1x_posterior.shape == (B, 6, 1) and model.KGain.shape == (B, 6, 5)
     assert model.h_Q.shape == (1, B, 128) and model.h_Sigma.shape == (1, B, 128) and model.h_S.shape == (1, B, 128)
@@ -130,15 +132,19 @@ def test_fused_runner_vs_oracle(gpu, B, T, groups, in_mult):
     assert np.abs(f0 - eager).max() <= t
 
 
-def test_fused_runner_vs_reference_goldens(gpu):
+@pytest.mark.parametrize("name", ["knet.npz", "knet_b37_t60_im10.npz"])
+def test_fused_runner_vs_reference_goldens(gpu, name):
+    """The fused whole-T graph against the reference module's posteriors: B=4 x T=20 (in_mult 5) and a ragged
+    B=37 x T=60 batch of the in_mult 10 architecture (tests/golden/gen_knet_golden.py)."""
     from trajectory_generation_amd.knet import KNetSequenceRunner
-    _, _, model = build(gpu)
-    B = G["y_norm"].shape[0]
-    y = torch.tensor(G["y_norm"], dtype=torch.float32, device=gpu)
-    u = torch.tensor(G["u"], dtype=torch.float32, device=gpu)
-    m1x0 = torch.tensor(G["m1x0"], dtype=torch.float32, device=gpu)
+    g = np.load("tests/golden/" + name)
+    _, _, model = build(gpu, seed=int(g["seed"]), in_mult=int(g["in_mult"]), g=g)
+    B = g["y_norm"].shape[0]
+    y = torch.tensor(g["y_norm"], dtype=torch.float32, device=gpu)
+    u = torch.tensor(g["u"], dtype=torch.float32, device=gpu)
+    m1x0 = torch.tensor(g["m1x0"], dtype=torch.float32, device=gpu)
     post = KNetSequenceRunner(model, B).run(y, u, m1x0, fused=True).cpu().numpy()
-    assert np.abs(post - G["x_post"]).max() <= tol(G["x_post"])
+    assert np.abs(post - g["x_post"]).max() <= tol(g["x_post"])
 
 
 def test_ekf_vs_oracle_and_filters(gpu):
