@@ -600,10 +600,30 @@ def main(argv=None, ops_factory=None, backend=None):
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries the one JSON line only: what libraries print there while the bench runs (RCCL prints its
+    # version banner to stdout when a communicator is created) is routed to stderr until the line is written
+    sys.stdout.flush()
+    saved_stdout = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        out = _main_ranked(args, ops_factory, backend, world_env, rank, local)
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved_stdout, 1)
+        os.close(saved_stdout)
+    if out is not None:
+        print(json.dumps(out), flush=True)
+    return out
+
+
+def _main_ranked(args, ops_factory, backend, world_env, rank, local):
+    """This rank's process group (if any), device side and bench; rank 0 returns the record."""
     dist = None
     world = 1
     backend = backend or os.environ.get("TRAJ_BENCH_BACKEND", "nccl")
-    if world_env > 1:
+    # TRAJ_BENCH_PG=1: a process group even at world size 1 (exercises the RCCL rendezvous, the barriers and the
+    # MAX all-reduce on a one-GPU box -- tools/r03_rccl.sh; the driver's N = 1 run does not set it)
+    if world_env > 1 or os.environ.get("TRAJ_BENCH_PG") == "1":
         import datetime
         import torch.distributed as dist
         kw = {}
@@ -619,8 +639,6 @@ def main(argv=None, ops_factory=None, backend=None):
     finally:
         if dist:
             dist.destroy_process_group()
-    if out is not None:
-        print(json.dumps(out), flush=True)
     return out
 
 
