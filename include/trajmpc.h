@@ -43,7 +43,8 @@
 extern "C" {
 #endif
 
-#define TRAJMPC_ABI_VERSION 2   /* 2: traj_mpc_qp_batch takes a workspace; traj_mpc_sb_workspace_bytes */
+#define TRAJMPC_ABI_VERSION 3   /* 2: traj_mpc_qp_batch takes a workspace; traj_mpc_sb_workspace_bytes;
+                                  * 3: the step / QP entry points take horizons up to TRAJ_MAX_N_GENERAL */
 
 /* error codes (return values) */
 #define TRAJ_OK 0
@@ -69,7 +70,9 @@ typedef struct {
 /* mpc_step keyword arguments (mpc_6stati.py:120-143) + QP solver settings.  Solver defaults are
  * CVXPY's OSQP settings (eps_abs = eps_rel = 1e-5, max_iter = 10000, polish on). */
 typedef struct {
-    int N;                            /* horizon, 1 <= N <= TRAJ_MAX_N */
+    int N;                            /* horizon: 1 <= N <= TRAJ_MAX_N for every entry point; the step / QP
+                                       * entry points also take TRAJ_MAX_N < N <= TRAJ_MAX_N_GENERAL (general
+                                       * solver, caller-owned scratch: traj_mpc_sb_workspace_bytes) */
     double Ts;                        /* sampling time */
     double q_c, q_phi, q_vx;          /* :128-131 */
     double R[4], Rd[4];               /* :132-133, 2x2 row-major; the symmetric part is used */
@@ -91,7 +94,14 @@ typedef struct {
                                        * (mpc_6stati.py:256 requests warm_start=True) */
 } traj_mpc_config;
 
+/* Horizon tiers (mpc_step takes any N, mpc_6stati.py:125):
+ *   N <= TRAJ_MAX_N (40)                 the register-resident hot kernels (mpc_solve.h): every entry point;
+ *   TRAJ_MAX_N < N <= TRAJ_MAX_N_GENERAL the general condensed-QP solver (mpc_general.h, one 256-thread workgroup
+ *                                        per instance, its Cholesky factor in the caller's scratch): the step and
+ *                                        QP entry points only (traj_mpc_step_batch / traj_mpc_qp_batch); the
+ *                                        closed-loop entry points return TRAJ_E_UNSUPPORTED. */
 #define TRAJ_MAX_N 40
+#define TRAJ_MAX_N_GENERAL 256
 
 int traj_abi_version(void);
 const char* traj_status_string(int status);
@@ -122,9 +132,10 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
  * closed-loop solve order (B ints, longest first) and the fused run's step queue (B + 2 ints).  Pass the same buffer to every traj_closed_loop_step of one run;
  * step t = 0 starts cold. */
 size_t traj_mpc_workspace_bytes(int B, int N);
-/* Scratch of the state-bound solver (x_lo / x_hi given with a finite side, mpc_6stati.py:208-213): B * ~20.5k
- * doubles at N = 20.  traj_mpc_step_batch with state bounds needs traj_mpc_workspace_bytes(B, N) + this many
- * bytes; traj_mpc_qp_batch with state bounds needs this many.  0 for B < 0 or N out of range. */
+/* Scratch of the general solver, which runs with state bounds (x_lo / x_hi given with a finite side,
+ * mpc_6stati.py:208-213) and for every horizon N > TRAJ_MAX_N: B * ~20.5k doubles at N = 20 (N > TRAJ_MAX_N adds
+ * the Cholesky factor, 4 N^2 doubles).  traj_mpc_step_batch then needs traj_mpc_workspace_bytes(B, N) + this many
+ * bytes; traj_mpc_qp_batch this many.  0 for B < 0 or N outside 1 .. TRAJ_MAX_N_GENERAL. */
 size_t traj_mpc_sb_workspace_bytes(int B, int N);
 
 /* ---- the MPC step (mpc_6stati.py:120-275) for B independent instances ----
@@ -132,7 +143,7 @@ size_t traj_mpc_sb_workspace_bytes(int B, int N);
  * caller, :155-160).  Outputs: u_cmd [B,2], status [B]; optional (may be NULL): objective [B],
  * X_opt [B,6,N+1], U_opt [B,2,N], iters [B] (ADMM iterations), polished [B] (1 if polish accepted).
  * workspace: device buffer of at least traj_mpc_workspace_bytes(B, N) bytes (+ traj_mpc_sb_workspace_bytes(B, N)
- * with state bounds). */
+ * with state bounds or N > TRAJ_MAX_N). */
 int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                         const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
                         int* status, double* objective, double* X_opt, double* U_opt, int* iters, int* polished,
@@ -140,7 +151,7 @@ int traj_mpc_step_batch(const traj_vehicle_params* p, const traj_mpc_config* c, 
 
 /* QP half only (mpc_6stati.py:180-275) with the linearization supplied by the caller:
  * Ad [B,N,6,6], Bd [B,N,6,2], g [B,N,6].  Same outputs as traj_mpc_step_batch.  workspace: only with state
- * bounds (>= traj_mpc_sb_workspace_bytes(B, N) bytes), otherwise may be NULL. */
+ * bounds or N > TRAJ_MAX_N (>= traj_mpc_sb_workspace_bytes(B, N) bytes), otherwise may be NULL. */
 int traj_mpc_qp_batch(const traj_vehicle_params* p, const traj_mpc_config* c, int B, const double* x0,
                       const double* u_prev, const double* path_ref, const double* vref, const double* Ad,
                       const double* Bd, const double* g, double* u_cmd, int* status, double* objective,
@@ -240,9 +251,9 @@ int traj_debug_spin_limit(int polls);
  * level order).  Results do not depend on it.  For experiments and tests. */
 int traj_debug_queue_lead(int steps, int per_mille);
 /* Fused-run kernel instance, by waves per SIMD: 0 (default) = by capacity and launch length (capacity 40: 2, or
- * 3 from 200 steps on; capacity 80: 1); 1, 2 or 3 = forced where built (capacity 40: 2 and 3; capacity 80: 1
- * and the lean two-wave instance at 2; otherwise the default).  Results do not depend on it (the instances are
- * bit-identical).  For experiments and tests. */
+ * 3 from 200 steps on; capacity 80: 1); 1, 2 or 3 = forced where built (capacity 40: 2 and 3; capacity 80: 2 runs
+ * the lean two-wave instance, 1 and 3 the default one-wave-per-SIMD instance; other capacities: the default).
+ * Results do not depend on it (the instances are bit-identical).  For experiments and tests. */
 int traj_debug_fused_waves(int waves);
 int traj_debug_kernel_times(double* ms, int* n_steps);
 

@@ -81,7 +81,7 @@ def test_struct_layout_matches_c(tmp_path):
 
 
 def test_abi_version_and_strings(L):
-    assert L.traj_abi_version() == 2
+    assert L.traj_abi_version() == 3
     for code, s in _lib.STATUS_STRINGS.items():
         assert L.traj_status_string(code).decode() == s
     for rc in (_lib.TRAJ_OK, _lib.TRAJ_E_ARG, _lib.TRAJ_E_UNSUPPORTED, _lib.TRAJ_E_LAUNCH):
@@ -126,10 +126,12 @@ def test_state_bound_workspace_bytes(L):
     """The state-bound solver's scratch is caller-owned (mpc_general.h gen_ws_doubles per instance)."""
     def per(N):
         n, m = 2 * N, 10 * N
-        return n * n + m * n + 6 * (N + 1) * n + 6 * (N + 1) + 3 * n + 20 * n + 24 * m + 64
-    for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40)):
+        return (n * n + m * n + 6 * (N + 1) * n + 6 * (N + 1) + 3 * n + 20 * n + 24 * m + 64 +
+                (n * n if N > _lib.MAX_N else 0))   # past the hot capacity the Cholesky factor leaves LDS
+    for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40), (3, 41), (2, 60), (1, _lib.MAX_N_GENERAL)):
         assert L.traj_mpc_sb_workspace_bytes(B, N) == B * per(N) * 8
-    assert L.traj_mpc_sb_workspace_bytes(-1, 20) == 0 and L.traj_mpc_sb_workspace_bytes(4, 41) == 0
+    assert L.traj_mpc_sb_workspace_bytes(-1, 20) == 0
+    assert L.traj_mpc_sb_workspace_bytes(4, _lib.MAX_N_GENERAL + 1) == 0
 
 
 def test_argument_errors_are_reported_before_any_launch(L):
@@ -141,12 +143,20 @@ def test_argument_errors_are_reported_before_any_launch(L):
     assert L.traj_mpc_step_batch(C.byref(p), C.byref(c), -1, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_E_ARG
     # empty batch is a no-op
     assert L.traj_mpc_step_batch(C.byref(p), C.byref(c), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_OK
-    # horizon beyond the compiled capacity / non-positive horizon
-    for N in (0, _lib.MAX_N + 1):
+    # horizon beyond the general solver's capacity / non-positive horizon
+    for N in (0, _lib.MAX_N_GENERAL + 1):
         cN = _lib.default_config(20, 0.05)
         cN.N = N
-        assert L.traj_mpc_step_batch(C.byref(p), C.byref(cN), 0, *([nul] * 11), nul, 0, nul) in (
-            _lib.TRAJ_E_ARG, _lib.TRAJ_E_UNSUPPORTED)
+        assert L.traj_mpc_step_batch(C.byref(p), C.byref(cN), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_E_ARG
+    # past the hot kernels' capacity: the step / QP entry points take it (general solver, caller-owned scratch:
+    # a workspace without it is refused before launching); the closed loop reports it as unsupported
+    cL = _lib.default_config(60, 0.05)
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cL), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_OK
+    fk = C.c_void_p(16)
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cL), 4, *([fk] * 11), fk,
+                                 L.traj_mpc_workspace_bytes(4, 60), nul) == _lib.TRAJ_E_ARG
+    assert L.traj_mpc_qp_batch(C.byref(p), C.byref(cL), 4, *([fk] * 14), nul, 0, nul) == _lib.TRAJ_E_ARG
+    assert L.traj_closed_loop_check(nul, 0, 4, 60, nul) == _lib.TRAJ_E_ARG
     # workspace too small (checked before launching)
     fake = C.c_void_p(16)
     args = [fake] * 11
@@ -168,6 +178,12 @@ def test_argument_errors_are_reported_before_any_launch(L):
     ps.kmax, ps.kind, ps.pc = 0, 16, 16                      # never dereferenced at B = 0
     assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 0, nul, nul, nul, 0, 0, nul, nul, nul,
                                    nul, nul, 0, nul) == _lib.TRAJ_E_UNSUPPORTED
+    # a horizon past the hot kernels' capacity: the closed loop reports it as unsupported, not as an argument error
+    cL = _lib.default_config(60, 0.05)
+    for fn in (L.traj_closed_loop_step, L.traj_closed_loop_run):
+        extra = (0, 1) if fn is L.traj_closed_loop_run else (0,)
+        assert fn(C.byref(p), C.byref(cL), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
+                  nul) == _lib.TRAJ_E_UNSUPPORTED
 
 
 def test_check_raises():

@@ -347,10 +347,12 @@ def test_closed_loop_history_matches_single_steps(gpu):
         assert np.array_equal(res["X"].cpu().numpy()[:, t + 1], x)
 
 
-@pytest.mark.parametrize("N,warm,mode", [(20, 1, 0), (20, 0, 0), (8, 1, 0), (40, 1, 0), (20, 1, 1)])
+@pytest.mark.parametrize("N,warm,mode", [(20, 1, 0), (20, 0, 0), (8, 1, 0), (12, 1, 0), (30, 1, 0), (40, 1, 0),
+                                         (20, 1, 1)])
 def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
     """traj_closed_loop_run (one launch, in-workgroup linearization, on-chip state) equals the per-step
-    launches bit for bit: histories, statuses, iteration counts; also when split into two runs."""
+    launches bit for bit: histories, statuses, iteration counts; also when split into two runs.  Every
+    capacity the compact fused image covers: 16 (N 8), 32 (N 12), 40 (N 20), 64 (N 30), 80 (N 40)."""
     from trajectory_generation_amd.workload import make_workload
     Ts, T, B = 0.05, 24, 96
     w = make_workload(B, N, Ts, kind="mixed" if N == 40 else "spline", seed=6)
@@ -518,6 +520,45 @@ def test_dropin_mpc_step_contract(gpu, oracle_lib):
     _, s6, i6 = M.mpc_step(x0[0], up[0], pr[0], Ts=0.05, N=20, params={"m": 0.05})
     assert s6 in ("optimal", "optimal_inaccurate")
     assert not np.array_equal(i6["U_opt"], info["U_opt"])
+
+
+@pytest.mark.parametrize("N,Ts,B", [(60, 0.02, 24), (41, 0.05, 16), (60, 0.05, 16)])
+def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
+    """Horizons past the hot kernels' capacity (TRAJ_MAX_N = 40) run the general condensed-QP solver with its
+    Cholesky factor in the caller's scratch (include/trajmpc.h horizon tiers): mpc_step takes any N
+    (mpc_6stati.py:125).  Batch entry point and the drop-in module against the oracle at the step tests' bars:
+    statuses identical, iteration counts equal on >= 95 %, U within 1e-6 where both polished and 1e-4 where
+    neither did; the drop-in returns the batch's u_cmd and the reference's fallback contract."""
+    from trajectory_generation_amd import mpc_6stati as M
+    g, r = _step_both(oracle_lib, 17, B, N, Ts, 0)
+    assert np.array_equal(g["status"], r["status"])
+    ok = g["status"] <= 1
+    assert ok.mean() >= 0.5
+    pg, pr = g["polished"] > 0, r["polished"] > 0
+    assert np.mean(pg == pr) >= 0.95 and np.mean(g["iters"] == r["iters"]) >= 0.95
+    du = np.abs(g["U_opt"] - r["U_opt"]).max(axis=(1, 2))
+    assert du[pg & pr & ok].max(initial=0.0) <= 1e-6
+    assert du[~pg & ~pr & ok].max(initial=0.0) <= 1e-4
+    assert np.array_equal(g["u_cmd"][ok], g["U_opt"][ok][:, :, 0])
+    assert g["X_opt"].shape == (B, 6, N + 1) and np.array_equal(g["X_opt"][ok][:, :, 0], random_instances(17, B, N, Ts)[0][ok])
+    # the drop-in module (the reference's per-call path) on the first instances
+    x0, up, pr_, vr = random_instances(17, B, N, Ts)
+    for b in range(3):
+        u, status, info = M.mpc_step(x0[b], up[b], pr_[b], Ts=Ts, N=N, vref=vr[b])
+        assert status == _lib_status(g["status"][b])
+        if g["status"][b] <= 1:
+            np.testing.assert_array_equal(u, g["u_cmd"][b])
+            assert info["X_opt"].shape == (6, N + 1) and info["U_opt"].shape == (2, N)
+        else:
+            assert np.array_equal(u, up[b]) and info == {}
+    d = M.mpc_step_batch(x0, up, pr_, vr, Ts=Ts, N=N)
+    assert np.array_equal(d["status"].cpu().numpy(), g["status"])
+    assert np.array_equal(d["u_cmd"].cpu().numpy(), g["u_cmd"])
+
+
+def _lib_status(code):
+    from trajectory_generation_amd._lib import STATUS_STRINGS
+    return STATUS_STRINGS[int(code)]
 
 
 # ------------------------------------------------------------------ state bounds (a9, :208-213)

@@ -17,7 +17,8 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "trajmpc.h")
 HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "trajknet.h")]
 
 TRAJ_OK, TRAJ_E_ARG, TRAJ_E_UNSUPPORTED, TRAJ_E_LAUNCH, TRAJ_E_HANDOFF = 0, -1, -2, -3, -4
-MAX_N = 40
+MAX_N = 40            # hot kernels, every entry point (include/trajmpc.h TRAJ_MAX_N)
+MAX_N_GENERAL = 256   # step / QP entry points on the general solver (TRAJ_MAX_N_GENERAL)
 
 STATUS_STRINGS = {
     0: "optimal",
@@ -169,7 +170,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.traj_abi_version() != 2:
+        if L.traj_abi_version() != 3:
             raise RuntimeError("libtrajmpc ABI version mismatch")
         _lib = L
     return _lib

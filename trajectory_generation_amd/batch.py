@@ -158,6 +158,12 @@ def _state_bounds(cfg: MpcConfig) -> bool:
     return any((cfg.has_x_lo and cfg.x_lo[i] > -1e30) or (cfg.has_x_hi and cfg.x_hi[i] < 1e30) for i in range(6))
 
 
+def _general(cfg: MpcConfig) -> bool:
+    """The step runs the general solver (caller-owned scratch, traj_mpc_sb_workspace_bytes): state bounds, or a
+    horizon past the hot kernels' capacity (MAX_N < N <= MAX_N_GENERAL, include/trajmpc.h's tiers)."""
+    return _state_bounds(cfg) or cfg.N > _lib.MAX_N
+
+
 def workspace(B: int, N: int, device, extra_bytes: int = 0, role: str = "closed_loop") -> torch.Tensor:
     """Cached device workspace for B instances of horizon N (traj_mpc_workspace_bytes), plus extra_bytes
     (traj_mpc_sb_workspace_bytes: the state-bound solver's scratch, caller-owned like the rest).
@@ -192,7 +198,7 @@ def mpc_step_batch(x0, u_prev, path_ref, vref, cfg: MpcConfig, params=None, out:
     path_ref = _dev(path_ref, (B, N + 1, 3), dev)
     vref = _dev(vref, (B, N + 1), dev)
     o = out if out is not None else _outputs(B, N, dev)
-    sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _state_bounds(cfg) else 0
+    sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _general(cfg) else 0
     ws = workspace(B, N, dev, sb, role="step")
     _lib.check(_lib.lib().traj_mpc_step_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), _p(u_prev), _p(path_ref), _p(vref),
@@ -210,7 +216,7 @@ def mpc_qp_batch(x0, u_prev, path_ref, vref, Ad, Bd, g, cfg: MpcConfig, params=N
     args = [_dev(u_prev, (B, 2), dev), _dev(path_ref, (B, N + 1, 3), dev), _dev(vref, (B, N + 1), dev),
             _dev(Ad, (B, N, 6, 6), dev), _dev(Bd, (B, N, 6, 2), dev), _dev(g, (B, N, 6), dev)]
     o = _outputs(B, N, dev)
-    sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _state_bounds(cfg) else 0
+    sb = int(_lib.lib().traj_mpc_sb_workspace_bytes(B, N)) if _general(cfg) else 0
     ws = workspace(0, N, dev, sb, role="step") if sb else None
     _lib.check(_lib.lib().traj_mpc_qp_batch(
         C.byref(params_struct(params)), C.byref(cfg), B, _p(x0), *[_p(a) for a in args],

@@ -16,9 +16,10 @@
 //     oracle's chol_solve adds them (ascending k forward, descending k backward);
 //   * -ffp-contract=off on both sides; division and sqrt are IEEE-rounded.
 // Layout: one 256-thread workgroup per instance; the Cholesky factor lives in LDS (n <= 80:
-// 51 KB); everything else in the caller's workspace: traj_mpc_sb_workspace_bytes(B, N) bytes past the step's
-// workspace (traj_mpc_step_batch) or the workspace argument of traj_mpc_qp_batch (ABI 2; the library never
-// allocates).  This path is for the optional argument only -- correctness first;
+// 51 KB) or, for the horizons past the hot kernels' capacity (TRAJ_MAX_N < N <= TRAJ_MAX_N_GENERAL), in the
+// caller's scratch; everything else in the caller's workspace: traj_mpc_sb_workspace_bytes(B, N) bytes past the
+// step's workspace (traj_mpc_step_batch) or the workspace argument of traj_mpc_qp_batch (the library never
+// allocates).  This path is for the optional argument and the long horizons only -- correctness first;
 // the 4096-trajectory closed loop never takes it.
 #pragma once
 #include "mpc_common.h"
@@ -26,15 +27,18 @@
 namespace tgmpc {
 
 constexpr int GEN_NT = 256;
-constexpr int GEN_NMAX = 2 * TRAJ_MAX_N;
+constexpr int GEN_NMAX = 2 * TRAJ_MAX_N;                    // n whose Cholesky factor is kept in LDS
+constexpr int GEN_RMAX = (2 * TRAJ_MAX_N_GENERAL + 63) / 64;  // rows per lane of the one-wave triangular solves
 
-// per-instance scratch of solve_gen_kernel, in doubles (m <= 10 N rows)
+// per-instance scratch of solve_gen_kernel, in doubles (m <= 10 N rows; n > GEN_NMAX: + the n x n factor)
 __host__ __device__ inline size_t gen_ws_doubles(int N) {
     const size_t n = 2 * (size_t)N, m = 10 * (size_t)N;
-    return n * n + m * n + 6 * (size_t)(N + 1) * n + 6 * (size_t)(N + 1) + 3 * n + 20 * n + 24 * m + 64;
+    return n * n + m * n + 6 * (size_t)(N + 1) * n + 6 * (size_t)(N + 1) + 3 * n + 20 * n + 24 * m + 64 +
+           (n > (size_t)GEN_NMAX ? n * n : 0);
 }
 
 struct GenWs {
+    double *L;   // the Cholesky factor when it does not fit LDS (n > GEN_NMAX), else null
     double *P, *A, *G, *xh, *F;
     double *q, *D, *Dinv, *Dt, *x, *xt, *xp, *rhs, *Px, *Aty, *xpol, *r1, *tt, *xs, *U;   // n
     double *l, *u, *E, *Einv, *Et, *rv, *ri, *z, *y, *zt, *zp, *yp, *tm2, *Ax, *zpol, *ypol, *bb, *r2, *dd,
@@ -60,6 +64,7 @@ __device__ inline GenWs gen_carve(double* p, int N) {
     double** vm[] = {&w.l, &w.u, &w.E, &w.Einv, &w.Et, &w.rv, &w.ri, &w.z, &w.y, &w.zt, &w.zp, &w.yp, &w.tm2,
                      &w.Ax, &w.zpol, &w.ypol, &w.bb, &w.r2, &w.dd, &w.act, &w.rvp};
     for (double** v : vm) *v = take(m);
+    w.L = (n > (size_t)GEN_NMAX) ? take(n * n) : nullptr;
     return w;
 }
 
@@ -119,9 +124,10 @@ __device__ inline void gen_mtv(const double* M, int r, int cdim, const double* x
 }
 
 // K = P + sig I + A' diag(rv) A (lower triangle, factor_kkt's per-entry order) then Cholesky in place
-// (lower factor in L[i * LD + j], i >= j).  Returns false if a pivot is not positive.
+// (lower factor in L[i * LD + j], i >= j; LD = GEN_LD in LDS, n in the caller's scratch).  Returns false if a
+// pivot is not positive.
 constexpr int GEN_LD = GEN_NMAX + 1;
-__device__ inline bool gen_factor(const GenWs& w, const double* rv, int n, int m, double sig, double* L,
+__device__ inline bool gen_factor(const GenWs& w, const double* rv, int n, int m, double sig, double* L, int LD,
                                   int* s_ok) {
     const int t = threadIdx.x;
     for (int e = t; e < n * n; e += GEN_NT) {
@@ -137,20 +143,20 @@ __device__ inline bool gen_factor(const GenWs& w, const double* rv, int n, int m
             const double tq = rr * a[i];
             k += tq * a[j];
         }
-        L[i * GEN_LD + j] = k;
+        L[i * LD + j] = k;
     }
     if (t == 0) *s_ok = 1;
     __syncthreads();
     for (int j = 0; j < n; ++j) {
         if (t == 0) {
-            const double s = L[j * GEN_LD + j];
+            const double s = L[j * LD + j];
             if (!(s > 0.0)) *s_ok = 0;
-            else L[j * GEN_LD + j] = sqrt(s);
+            else L[j * LD + j] = sqrt(s);
         }
         __syncthreads();
         if (!*s_ok) return false;
-        const double d = L[j * GEN_LD + j];
-        for (int i = j + 1 + t; i < n; i += GEN_NT) L[i * GEN_LD + j] = L[i * GEN_LD + j] / d;
+        const double d = L[j * LD + j];
+        for (int i = j + 1 + t; i < n; i += GEN_NT) L[i * LD + j] = L[i * LD + j] / d;
         __syncthreads();
         // trailing update: entry (i, c), i >= c > j, minus L[i][j] L[c][j]
         const int nr = n - j - 1;
@@ -158,45 +164,51 @@ __device__ inline bool gen_factor(const GenWs& w, const double* rv, int n, int m
             const int ii = e / nr, cc = e - ii * nr;
             if (cc > ii) continue;
             const int i = j + 1 + ii, c = j + 1 + cc;
-            L[i * GEN_LD + c] -= L[i * GEN_LD + j] * L[c * GEN_LD + j];
+            L[i * LD + c] -= L[i * LD + j] * L[c * LD + j];
         }
         __syncthreads();
     }
     return true;
 }
 
-// b <- K^{-1} b with the factor L (chol_solve): wave 0, lane l owns rows l and l + 64
-__device__ inline void gen_solve(const double* L, int n, double* b) {
+// b <- K^{-1} b with the factor L (chol_solve): wave 0, lane l owns rows l, l + 64, l + 128, ... (GEN_RMAX)
+__device__ inline void gen_solve(const double* L, int LD, int n, double* b) {
     const int t = threadIdx.x;
     if (t < 64) {
-        const int r0 = t, r1 = t + 64;
-        double t0 = r0 < n ? b[r0] : 0.0, t1 = r1 < n ? b[r1] : 0.0;
+        double v[GEN_RMAX];
+#pragma unroll
+        for (int r = 0; r < GEN_RMAX; ++r) v[r] = (t + 64 * r < n) ? b[t + 64 * r] : 0.0;
         for (int k = 0; k < n; ++k) {   // forward: row i's terms in ascending k
-            const bool hi = k >= 64;
-            const int owner = k & 63;
-            double v = hi ? t1 : t0;
-            if (t == owner) v = v / L[k * GEN_LD + k];
-            const double bk = __shfl(v, owner);
-            if (t == owner) {
-                if (hi) t1 = bk; else t0 = bk;
+            const int owner = k & 63, kr = k >> 6;
+            double x = 0.0;
+#pragma unroll
+            for (int r = 0; r < GEN_RMAX; ++r) x = (r == kr) ? v[r] : x;
+            if (t == owner) x = x / L[k * LD + k];
+            const double bk = __shfl(x, owner);
+#pragma unroll
+            for (int r = 0; r < GEN_RMAX; ++r) {
+                const int row = t + 64 * r;
+                if (r == kr && t == owner) v[r] = bk;
+                if (row > k && row < n) v[r] -= L[row * LD + k] * bk;
             }
-            if (r0 > k && r0 < n) t0 -= L[r0 * GEN_LD + k] * bk;
-            if (r1 > k && r1 < n) t1 -= L[r1 * GEN_LD + k] * bk;
         }
         for (int k = n - 1; k >= 0; --k) {   // backward: row i's terms in descending k
-            const bool hi = k >= 64;
-            const int owner = k & 63;
-            double v = hi ? t1 : t0;
-            if (t == owner) v = v / L[k * GEN_LD + k];
-            const double bk = __shfl(v, owner);
-            if (t == owner) {
-                if (hi) t1 = bk; else t0 = bk;
+            const int owner = k & 63, kr = k >> 6;
+            double x = 0.0;
+#pragma unroll
+            for (int r = 0; r < GEN_RMAX; ++r) x = (r == kr) ? v[r] : x;
+            if (t == owner) x = x / L[k * LD + k];
+            const double bk = __shfl(x, owner);
+#pragma unroll
+            for (int r = 0; r < GEN_RMAX; ++r) {
+                const int row = t + 64 * r;
+                if (r == kr && t == owner) v[r] = bk;
+                if (row < k) v[r] -= L[k * LD + row] * bk;
             }
-            if (r0 < k) t0 -= L[k * GEN_LD + r0] * bk;
-            if (r1 < k && r1 < n) t1 -= L[k * GEN_LD + r1] * bk;
         }
-        if (r0 < n) b[r0] = t0;
-        if (r1 < n) b[r1] = t1;
+#pragma unroll
+        for (int r = 0; r < GEN_RMAX; ++r)
+            if (t + 64 * r < n) b[t + 64 * r] = v[r];
     }
     __syncthreads();
 }
@@ -299,7 +311,7 @@ __device__ inline void gen_active(const GenWs& w, int m, const double* z, const 
 }
 
 // reduced-KKT solve for the active set w.act (kkt_solve_active): x -> w.xpol, y -> w.ypol, A x -> w.Ax
-__device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, int n, int m, double* L,
+__device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, int n, int m, double* L, int LD,
                                       int* s_ok) {
     const int t = threadIdx.x;
     const double dlt = c.delta;
@@ -309,7 +321,7 @@ __device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, 
         w.rvp[i] = (a != 0.0) ? 1.0 / dlt : 0.0;
     }
     __syncthreads();
-    if (!gen_factor(w, w.rvp, n, m, dlt, L, s_ok)) return false;
+    if (!gen_factor(w, w.rvp, n, m, dlt, L, LD, s_ok)) return false;
     for (int j = t; j < n; j += GEN_NT) {
         w.xpol[j] = 0.0;
         w.r1[j] = -w.q[j];
@@ -330,7 +342,7 @@ __device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, 
             w.tt[j] = s;
         }
         __syncthreads();
-        gen_solve(L, n, w.tt);
+        gen_solve(L, LD, n, w.tt);
         gen_mv(w.A, m, n, w.tt, w.Ax);
         __syncthreads();
         for (int j = t; j < n; j += GEN_NT) w.xpol[j] += w.tt[j];
@@ -361,6 +373,9 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
     const traj_mpc_config& c = a.c;
     const int N = c.N, n = 2 * N;
     const GenWs w = gen_carve(gws + (size_t)b * gstride, N);
+    // the factor: LDS up to the hot kernels' capacity, the caller's scratch past it
+    double* const s_Lf = (n <= GEN_NMAX) ? s_L : w.L;
+    const int LD = (n <= GEN_NMAX) ? GEN_LD : n;
     const double* x0 = a.x0 + 6 * (size_t)b;
     const double* up = a.u_prev + 2 * (size_t)b;
     const double* pref = a.path_ref + (size_t)3 * (N + 1) * b;
@@ -629,7 +644,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
             for (int i = t; i < m; i += GEN_NT) { w.z[i] = 0.0; w.y[i] = 0.0; }
             __syncthreads();
             set_rho();
-            if (gen_factor(w, w.rv, n, m, c.sigma, s_L, &s_i[3])) {
+            if (gen_factor(w, w.rv, n, m, c.sigma, s_Lf, LD, &s_i[3])) {
                 GenResid r = {};
                 int converged = 0, rounds = 0;
                 bool infeasible = false, fail = false;
@@ -648,7 +663,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                         __syncthreads();
                         for (int j = t; j < n; j += GEN_NT) w.xt[j] = w.rhs[j] + (c.sigma * w.xp[j] - w.q[j]);
                         __syncthreads();
-                        gen_solve(s_L, n, w.xt);
+                        gen_solve(s_Lf, LD, n, w.xt);
                         gen_mv(w.A, m, n, w.xt, w.zt);
                         __syncthreads();
                         for (int j = t; j < n; j += GEN_NT) w.x[j] = c.alpha * w.xt[j] + (1.0 - c.alpha) * w.xp[j];
@@ -679,7 +694,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                                 if (est > rho * c.adaptive_rho_tol || est < rho / c.adaptive_rho_tol) {
                                     rho = est;
                                     set_rho();
-                                    if (!gen_factor(w, w.rv, n, m, c.sigma, s_L, &s_i[3])) { fail = true; break; }
+                                    if (!gen_factor(w, w.rv, n, m, c.sigma, s_Lf, LD, &s_i[3])) { fail = true; break; }
                                 }
                             }
                         }
@@ -703,7 +718,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                         int cert = 0, pass;
                         const double tol = c.cert_tol;
                         for (pass = 1; pass <= c.polish_max_pass; ++pass) {
-                            if (!gen_kkt_active(w, c, n, m, s_L, &s_i[3])) break;
+                            if (!gen_kkt_active(w, c, n, m, s_Lf, LD, &s_i[3])) break;
                             gen_mv(w.P, n, n, w.xpol, w.Px);
                             gen_mtv(w.A, m, n, w.ypol, w.Aty);
                             __syncthreads();
@@ -747,7 +762,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                             converged = 0;
                             ++iter;
                             set_rho();   // the ADMM factor (the polish overwrote it): same rho, same bits
-                            if (!gen_factor(w, w.rv, n, m, c.sigma, s_L, &s_i[3])) {
+                            if (!gen_factor(w, w.rv, n, m, c.sigma, s_Lf, LD, &s_i[3])) {
                                 status = TRAJ_STATUS_SOLVER_ERROR;
                                 break;
                             }
@@ -756,7 +771,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                     } else if (status == TRAJ_STATUS_OPTIMAL && c.polish) {
                         // osqp_polish + OSQP's acceptance rule
                         gen_active(w, m, w.z, w.y);
-                        if (gen_kkt_active(w, c, n, m, s_L, &s_i[3])) {
+                        if (gen_kkt_active(w, c, n, m, s_Lf, LD, &s_i[3])) {
                             for (int i = t; i < m; i += GEN_NT) {
                                 const double ztv = w.Ax[i] + w.ypol[i];
                                 const double zz = ztv < w.l[i] ? w.l[i] : (ztv > w.u[i] ? w.u[i] : ztv);

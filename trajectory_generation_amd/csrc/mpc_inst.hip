@@ -25,9 +25,10 @@ int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
         if (a.wps == 3) return launch_fused_w3_40(a, st);
 #endif
 #if TGMPC_NN > 64
-        // capacity 80: the lean two-wave instance (2 waves per SIMD, 4 instances per CU) unless one wave per
-        // SIMD is asked for (traj_debug_fused_waves(1): the instance with the whole pivot row in registers)
-        if (a.wps == 1) return launch_fused<NN, 1>(a, st);
+        // capacity 80: one wave per SIMD (the default, a.wps = 1) unless the lean two-wave instance (2 waves per
+        // SIMD, 4 instances per CU, opt-in) is asked for with traj_debug_fused_waves(2); any other value runs the
+        // default
+        if (a.wps != 2) return launch_fused<NN, 1>(a, st);
 #endif
         return launch_fused<NN, 2>(a, st);
     }

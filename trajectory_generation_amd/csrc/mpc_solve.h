@@ -40,9 +40,9 @@
 #endif
 #ifndef TGMPC_PCH
 #define TGMPC_PCH 4            // CMP: pivot-row double2 per chunk of the sweep
+#endif
 #ifndef TGMPC_NSTASH
 #define TGMPC_NSTASH 3         // 3-wave instance: ADMM iterate rows parked in LDS across the factorization (of 5)
-#endif
 #endif
 #ifndef TGMPC_L2W_WPE
 #define TGMPC_L2W_WPE 2        // waves per SIMD the lean two-wave instance is built for
@@ -87,6 +87,9 @@
 #endif
 #ifndef TGMPC_RECV2_L2W
 #define TGMPC_RECV2_L2W 1      // L2W: the receiver sweep as well (scratch 1,864 -> 396 B/lane; still opt-in)
+#endif
+#ifndef TGMPC_COND_SPARSE
+#define TGMPC_COND_SPARSE 1    // closed loop: the condensing skips A_k's structural zeros and P's all-zero MFMA tiles
 #endif
 
 namespace tgmpc {
@@ -542,18 +545,41 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             for (int j = 0; j < NN; ++j) Prow[j] = 0.0;
         }
         const int mr = (t >> 4) & 3, mc = t & 15;   // MFMA operand slot of this lane: k-row, column
+        // Row r of A_k x (+ v0) as the chain v = fma(A[r][cc], x[cc], v), cc = 0..5.  In the closed loop A_k comes
+        // from the in-library linearization, whose structural entries are exact (mpc_linearize.h: f does not read
+        // X, Y; f_0, f_1 do not read omega; f_2 = omega; f_3..5 do not read phi -- the central differences of those
+        // columns are exactly 0, so A = I + Ts J holds exact 1s and 0s there): rows 0 / 1 = [1 0 a a a 0] /
+        // [0 1 a a a 0], row 2 = [0 0 1 0 0 a], rows 3..5 = [0 0 0 a a a].  The chain then skips the zero terms
+        // and adds the unit ones (fma(1, x, v) = v + x, fma(0, x, v) = v for finite x): the same values (up to
+        // the sign of a zero) with 16 fmas and 3 adds instead of 36 fmas.  The QP entry point (caller's A_k) and
+        // the step keep the full chain.
+        constexpr bool SPARSE_A = CLOSED && TGMPC_COND_SPARSE;
+        auto arow = [&](const double* Ak, int r, const double* x, double v) -> double {
+            if constexpr (SPARSE_A) {
+                if (r <= 1) {
+                    v = v + x[r];
+#pragma unroll
+                    for (int cc = 2; cc < 5; ++cc) v = fma(Ak[6 * r + cc], x[cc], v);
+                } else if (r == 2) {
+                    v = v + x[2];
+                    v = fma(Ak[6 * 2 + 5], x[5], v);
+                } else {
+#pragma unroll
+                    for (int cc = 3; cc < 6; ++cc) v = fma(Ak[6 * r + cc], x[cc], v);
+                }
+            } else {
+#pragma unroll
+                for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], x[cc], v);
+            }
+            return v;
+        };
         for (int k = 0; k < N; ++k) {
             const double* Ak = cA + RA * k;
             if constexpr (!FREE_LANE) {
                 // free response xh_{k+1} = A_k xh_k + g_k (uniform)
                 double xn[6];
 #pragma unroll
-                for (int r = 0; r < 6; ++r) {
-                    double v = cg[RG * k + r];
-#pragma unroll
-                    for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], xh[cc], v);
-                    xn[r] = v;
-                }
+                for (int r = 0; r < 6; ++r) xn[r] = arow(Ak, r, xh, cg[RG * k + r]);
 #pragma unroll
                 for (int r = 0; r < 6; ++r) xh[r] = xn[r];
             }
@@ -566,9 +592,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 double Gn[6];
 #pragma unroll
                 for (int r = 0; r < 6; ++r) {
-                    double v = fl ? cg[RG * k + r] : 0.0;
-#pragma unroll
-                    for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * r + cc], G[cc], v);
+                    const double v = arow(Ak, r, G, fl ? cg[RG * k + r] : 0.0);
                     const double bv = cB[RB * k + 2 * r + ch];
                     Gn[r] = prop ? v : (enter ? bv : G[r]);
                 }
@@ -600,6 +624,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #pragma unroll
                 for (int ib = 0; ib < NB; ++ib) opv[ib] = fb[mr * FS + 16 * ib + mc];
 #endif
+                // F_k's columns >= 2 (k + 1) are exact zeros (the inputs of later stages): a tile whose column block
+                // starts there adds +-0 to its accumulator and is skipped (bit-identical; stages 0..7 touch one
+                // tile of 6 at capacity 40, 56 MFMAs per instance instead of 120 at N = 20)
                 int ti = 0;
 #pragma unroll
                 for (int ib = 0; ib < NB; ++ib)
@@ -608,7 +635,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #ifdef TGMPC_EXP_NO_MFMA
                         acc[ti][0] += opv[ib] * opv[jb];
 #else
-                        acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(opv[ib], opv[jb], acc[ti], 0, 0, 0);
+                        if (!TGMPC_COND_SPARSE || 16 * jb < 2 * k + 2)
+                            acc[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(opv[ib], opv[jb], acc[ti], 0, 0, 0);
 #endif
             } else {
                 double* buf = s_ex + (xb & 1) * 3 * NN;   // 2 rotating slots of 3*NN
@@ -797,11 +825,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         for (int j = 0; j < NN; ++j) Prow[j] *= cs;
         qi *= cs;
         const double csinv = uniformize(1.0 / cs);   // uniform (held in SGPRs, not in VGPRs)
-        const double D_dn = exch(D, -2), Er_up = exch(Er, +2);
+        const double D_dn = exch(D, -2);
         // (a_rp(t) = Er(t+2) D(t) is a_rm(t+2) bit for bit: where it is needed it is taken from lane t+2 --
         // exch(a_rm, +2), or the product a_rm w formed on lane t+2 -- instead of living in a register)
         double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0;   // (CMP: re-formed, see reload)
-        (void)Er_up;
         // Cold per-lane values go to LDS and are re-read (volatile: never hoisted into registers)
         // where needed -- residual checks, the K build, polish, the ADMM loop's clamps -- keeping the ADMM
         // loop's live set down to the inverse row + ~12 doubles.  Single rows: D, E_box, E_rate, a_r(t+2), q.

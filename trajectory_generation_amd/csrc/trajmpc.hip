@@ -205,10 +205,12 @@ static bool state_bounds_active(const traj_mpc_config* c) {
     return false;
 }
 
-// allow_sb: the caller can run the general (state-bound) solver; the closed-loop entry points cannot
+// allow_sb: the caller can run the general solver (state bounds, horizons past TRAJ_MAX_N); the closed-loop
+// entry points cannot
 static int check_cfg(const traj_mpc_config* c, bool allow_sb = false) {
     if (!c) return TRAJ_E_ARG;
-    if (c->N < 1 || c->N > TRAJ_MAX_N) return TRAJ_E_ARG;
+    if (c->N < 1 || c->N > TRAJ_MAX_N_GENERAL) return TRAJ_E_ARG;
+    if (c->N > TRAJ_MAX_N && !allow_sb) return TRAJ_E_UNSUPPORTED;
     if (!(c->Ts > 0.0) || c->max_iter < 1 || c->check_interval < 1 || c->scaling_iters < 0) return TRAJ_E_ARG;
     if (c->polish_mode != 0 && c->polish_mode != 1) return TRAJ_E_ARG;
     if (!allow_sb && state_bounds_active(c)) return TRAJ_E_UNSUPPORTED;
@@ -440,7 +442,8 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (B == 0) return TRAJ_OK;
     if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
     if (!lin && (!Ad || !Bd || !g)) return TRAJ_E_ARG;
-    const bool sb = state_bounds_active(c);
+    // the general solver: state bounds, or a horizon past the hot kernels' capacity (include/trajmpc.h tiers)
+    const bool sb = state_bounds_active(c) || c->N > TRAJ_MAX_N;
     const size_t base = lin ? ws_base_bytes(B, c->N) : 0;
     const size_t need = base + (sb ? traj_mpc_sb_workspace_bytes(B, c->N) : 0);
     if (need > 0 && (!ws || ws_bytes < need)) return TRAJ_E_ARG;
@@ -477,7 +480,7 @@ size_t traj_mpc_workspace_bytes(int B, int N) {
 }
 
 size_t traj_mpc_sb_workspace_bytes(int B, int N) {
-    if (B < 0 || N < 1 || N > TRAJ_MAX_N) return 0;
+    if (B < 0 || N < 1 || N > TRAJ_MAX_N_GENERAL) return 0;
     return (size_t)B * gen_ws_doubles(N) * sizeof(double);
 }
 

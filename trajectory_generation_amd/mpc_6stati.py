@@ -20,6 +20,9 @@ reference; every computation runs in the HIP kernels of libtrajmpc.so on the GPU
   * any other status -> (u_prev, status, {})  (:261-262); a solver failure ->
     (u_prev, "Solver Error: <Exception>", {})  (:257-259).
   * `solver` is accepted and ignored (the QP is solved by the HIP ADMM); `verbose` is ignored.
+  * any horizon up to 256 (the reference takes any N, :125): N <= 40 runs the register-resident hot
+    kernels, 40 < N <= 256 the general condensed-QP solver (same OSQP restatement, slower; see
+    INTEGRATION.md "Horizon tiers").
 The QP's optimum is unique (R > 0), so the result is the one OSQP returns when its polish
 succeeds; see DESIGN.md "Parity" for the stated tolerances.
 """
@@ -75,6 +78,10 @@ class _CallIO:
     def send(self):
         self.d_in.copy_(self.h_in, non_blocking=True)
 
+    def abort(self):
+        """A launch after send() raised: let the pending H2D copy from h_in finish before anyone writes h_in again."""
+        torch.cuda.current_stream(self.d_in.device).synchronize()
+
     def receive(self):
         self.h_out.copy_(self.d_out, non_blocking=True)
         torch.cuda.current_stream(self.d_out.device).synchronize()
@@ -110,9 +117,13 @@ def f_cont(x, u, p):
     io.a_in[:6] = x
     io.a_in[6:] = u
     io.send()
-    _b._lib.check(_b._lib.lib().traj_f_cont_batch(C.byref(_b.params_struct(p)), 1, _b._p(io.d_in),
-                                                  C.c_void_p(io.d_in.data_ptr() + 48), _b._p(io.d_out), _b._stream()),
-                  "traj_f_cont_batch")
+    try:
+        _b._lib.check(_b._lib.lib().traj_f_cont_batch(C.byref(_b.params_struct(p)), 1, _b._p(io.d_in),
+                                                      C.c_void_p(io.d_in.data_ptr() + 48), _b._p(io.d_out),
+                                                      _b._stream()), "traj_f_cont_batch")
+    except BaseException:
+        io.abort()
+        raise
     return io.receive()[:6].copy()
 
 
@@ -218,8 +229,12 @@ def mpc_step(
     out = {"u_cmd": do[0:2].view(1, 2), "objective": do[2:3], "X_opt": do[3:3 + 6 * (N + 1)].view(1, 6, N + 1),
            "U_opt": do[3 + 6 * (N + 1):nf].view(1, 2, N), "status": ints[0:1], "iters": ints[1:2],
            "polished": ints[2:3]}
-    _b.mpc_step_batch(d[:6].view(1, 6), d[6:8].view(1, 2), d[8:8 + 3 * (N + 1)].view(1, N + 1, 3),
-                      d[8 + 3 * (N + 1):].view(1, N + 1), cfg, p, out=out)
+    try:
+        _b.mpc_step_batch(d[:6].view(1, 6), d[6:8].view(1, 2), d[8:8 + 3 * (N + 1)].view(1, N + 1, 3),
+                          d[8 + 3 * (N + 1):].view(1, N + 1), cfg, p, out=out)
+    except BaseException:
+        io.abort()
+        raise
     h = io.receive()
     st = int(h[nf:].view(np.int32)[0])
     status = STATUS_STRINGS.get(st, "Solver Error: SolverError")
