@@ -528,7 +528,7 @@ def dataset_leg(args, w, ops, dist, rank, world):
             Xa, Ua, sta = D.unpack_history(full)
             t3 = time.perf_counter()
             D._write_with_sidecar(os.path.join(args.dataset_csv, "vehicle_mpc"), Xa, Ua, sta, np.arange(Xa.shape[0]),
-                                  Ts, False)
+                                  Ts, True)
             csv_s = time.perf_counter() - t3
         bar()
         t4 = time.perf_counter()
@@ -540,14 +540,19 @@ def dataset_leg(args, w, ops, dist, rank, world):
     Xa, Ua, st = D.unpack_history(full)
     stn = st.cpu().numpy()
     n = world * B * T
+    n_failed = int(((stn >= D.FAILED_STATUS).sum(axis=0) > 0).sum())
     return {"what": "configs[3]: closed-loop dataset generation, histories gathered into rank 0",
             "trajectories": world * B, "steps": T, "traj_steps_per_s": n / gen_s, "generate_s": gen_s,
             "gather_s": gather_s, "gather_bytes": int(full.numel() * full.element_size()),
             "csv_s": csv_s, "csv_shards_s": shard_s,
-            "csv_note": "csv_s: rank 0 writes the gathered CSVs + status sidecar; csv_shards_s: every rank writes "
-                        "its own shard (no gather), max over ranks" if args.dataset_csv else None,
+            "csv_note": (f"{n_failed} of {world * B} trajectories have a failed step (status >= 2); the gathered CSV "
+                         "(dataset.generate's default, merge_datasets.py:41-47's filter) leaves them out and "
+                         "re-indexes the rest, its status sidecar keeps the generation ids"
+                         + ("; csv_s: rank 0 writes the gathered CSVs + status sidecar; csv_shards_s: every rank "
+                            "writes its own shard (no gather, failed ones flagged in the sidecar), max over ranks"
+                            if args.dataset_csv else "")),
             "status_hist": np.bincount(stn.reshape(-1).astype(np.int64), minlength=7).tolist(),
-            "failed_trajectories": int(((stn >= D.FAILED_STATUS).sum(axis=0) > 0).sum())}
+            "failed_trajectories": n_failed}
 
 
 def parse_args(argv=None):

@@ -64,7 +64,7 @@ def _worker(rank, world, port, q, out_prefix, shards=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     B, T = 4, 6
     r = D.generate(B, T, N=20, Ts=0.05, kind="spline", seed=3, out_prefix=out_prefix, dist=dist,
-                   closed_loop=_fake_closed_loop, shards=shards)
+                   closed_loop=_fake_closed_loop, shards=shards, drop_failed=False)
     if shards:
         q.put((rank, r[0].numpy(), r[1].numpy(), r[2].numpy()))
     elif rank == 0:
@@ -156,7 +156,8 @@ def test_status_sidecar_and_failed_trajectory_filter(tmp_path):
     import pandas as pd
     B, T = 6, 4
     p1 = str(tmp_path / "all")
-    X, U, st = D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p1, closed_loop=_status_closed_loop)
+    X, U, st = D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p1, closed_loop=_status_closed_loop,
+                          drop_failed=False)
     sc = pd.read_csv(p1 + "_status.csv")
     assert list(sc.columns) == ["trajectory_id", "source_id", "worst_status", "n_failed_steps", "first_failed_step"]
     assert sc["worst_status"].tolist() == [0, 1, 6, 0, 2, 0]
@@ -164,7 +165,7 @@ def test_status_sidecar_and_failed_trajectory_filter(tmp_path):
     assert sc["first_failed_step"].tolist() == [-1, -1, 1, -1, 3, -1]
     assert list(pd.read_csv(p1 + "_clean.csv").columns) == D.CLEAN_COLUMNS   # schema unchanged
     p2 = str(tmp_path / "ok")
-    D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p2, closed_loop=_status_closed_loop, drop_failed=True)
+    D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p2, closed_loop=_status_closed_loop)   # default: dropped
     sc2 = pd.read_csv(p2 + "_status.csv")
     assert sc2["trajectory_id"].tolist() == [0, 1, 2, 3] and sc2["source_id"].tolist() == [0, 1, 3, 5]
     assert (sc2["n_failed_steps"] == 0).all()

@@ -20,6 +20,10 @@
 #pragma once
 #include "physics.h"
 
+#ifndef TGMPC_DPP_BC
+#define TGMPC_DPP_BC 0   // DPP moves with bound_ctrl (see dpp_d)
+#endif
+
 namespace tgmpc {
 
 constexpr double INFTY = 1e30;
@@ -190,15 +194,18 @@ __device__ __forceinline__ void lds_load_all(const double* p, double (&o)[NN]) {
 template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ double dpp_d(double v) {
     int lo = __double2loint(v), hi = __double2hiint(v);
+#if TGMPC_DPP_BC
     if constexpr (ROW_MASK == 0xf) {
         // every row written: bound_ctrl gives the out-of-wave (or disabled) sources 0 -- the same values as an
-        // old operand of 0, without the two v_mov_b32 0 that initialise it
+        // old operand of 0, without the two v_mov_b32 0 that initialise it.  (Off by default: in the 3-wave
+        // instance it raised the scratch from 252 to 304 B/lane and cost a third of its 200-step rate.)
         lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, true);
         hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, true);
-    } else {
-        lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROW_MASK, 0xf, false);
-        hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROW_MASK, 0xf, false);
+        return __hiloint2double(hi, lo);
     }
+#endif
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROW_MASK, 0xf, false);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROW_MASK, 0xf, false);
     return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ double lane_up2(double v) { return dpp_d<0x130>(dpp_d<0x130>(v)); }  // lane t+2

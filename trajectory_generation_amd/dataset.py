@@ -135,15 +135,17 @@ def _closed_loop_gpu(w, T, cfg):
 
 
 def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=None, polish_mode=0,
-             closed_loop=None, drop_failed=False, shards=False):
+             closed_loop=None, drop_failed=None, shards=False):
     """Run the closed loop for this rank's B trajectories (ids rank * B .. rank * B + B - 1), gather the
     histories to rank 0 and (rank 0) write ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` and the
     status sidecar ``{out_prefix}_status.csv`` (write_status_csv).
 
     drop_failed: leave out every trajectory with a failed step (status >= 2) and re-index the rest 0..n-1 (the
-      ids data_loader.py expects, merge_datasets.py's re-indexing) -- each keeps the noise of its generation
-      id, which the sidecar's source_id column records.  Default False: every trajectory is written, the
-      sidecar flags the failed ones.
+      ids data_loader.py expects, merge_datasets.py:41-47's filter and re-indexing) -- each keeps the noise of its
+      generation id, which the sidecar's source_id column records.  Default (None): on with the gather, so a
+      diverged trajectory never lands silently in a training CSV; with shards=True (no gather to re-index
+      across ranks) every trajectory is written and the sidecar flags the failed ones.  False writes all of
+      them with the gather too (the reference generators' own behaviour).
     shards: no gather -- every rank writes its own ``{out_prefix}_rank{r}_*.csv`` (global ids; the shards'
       bodies concatenated in rank order are the single file's body) and its sidecar (SURVEY.md 8(e)'s
       per-rank alternative); returns this rank's share on every rank.
@@ -159,6 +161,8 @@ def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=N
         from . import batch as TB
         cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
         closed_loop = _closed_loop_gpu
+    if drop_failed is None:
+        drop_failed = not shards
     if shards and drop_failed:
         raise ValueError("drop_failed re-indexes the whole dataset: it needs the gather (shards=False)")
     res = closed_loop(w, T, cfg)
