@@ -21,7 +21,7 @@
 #include "physics.h"
 
 #ifndef TGMPC_DPP_BC
-#define TGMPC_DPP_BC 0   // DPP moves with bound_ctrl (see dpp_d)
+#define TGMPC_DPP_BC 0   // DPP moves with bound_ctrl (see dpp_d; the Makefile turns it on for mpc_inst.hip)
 #endif
 
 namespace tgmpc {
@@ -197,8 +197,8 @@ __device__ __forceinline__ double dpp_d(double v) {
 #if TGMPC_DPP_BC
     if constexpr (ROW_MASK == 0xf) {
         // every row written: bound_ctrl gives the out-of-wave (or disabled) sources 0 -- the same values as an
-        // old operand of 0, without the two v_mov_b32 0 that initialise it.  (Off by default: in the 3-wave
-        // instance it raised the scratch from 252 to 304 B/lane and cost a third of its 200-step rate.)
+        // old operand of 0, without the two v_mov_b32 0 that initialise it.  (Not in the 3-wave instance: there it
+        // raised the scratch from 252 to 304 B/lane and cost a third of its 200-step rate.)
         lo = __builtin_amdgcn_mov_dpp(lo, CTRL, 0xf, 0xf, true);
         hi = __builtin_amdgcn_mov_dpp(hi, CTRL, 0xf, 0xf, true);
         return __hiloint2double(hi, lo);

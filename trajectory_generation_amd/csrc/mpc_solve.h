@@ -88,6 +88,9 @@
 #ifndef TGMPC_RECV2_L2W
 #define TGMPC_RECV2_L2W 1      // L2W: the receiver sweep as well (scratch 1,864 -> 396 B/lane; still opt-in)
 #endif
+#ifndef TGMPC_FULLP
+#define TGMPC_FULLP 1          // one-wave, non-lean instances: the scaled P in LDS as the full symmetric matrix (row-major)
+#endif
 #ifndef TGMPC_COND_SPARSE
 #define TGMPC_COND_SPARSE 1    // closed loop: the condensing skips A_k's structural zeros and P's all-zero MFMA tiles
 #endif
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr int WAVES = (NN + 63) / 64;
     constexpr int NT = WAVES * 64;
     constexpr int NM = NN / 2;          // max horizon
-    constexpr int NP = NN * (NN + 1) / 2;
+    constexpr int NP0 = NN * (NN + 1) / 2;
 
     // CMP (fused, one wave): the compact LDS image -- at most 13 KB, so that 12 workgroups (3 waves per
     // SIMD) fit a CU's 160 KB.  One wave's LDS operations complete in program order, so buffers whose
@@ -137,6 +140,16 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr bool L2W = FUSED && WAVES == 2 && WPS >= 2;
     constexpr bool LEAN = (CMP && WPS >= 3) || L2W;
     static_assert(!L2W || CLOSED, "the lean two-wave instance is the fused closed loop");
+    // FULLP: the scaled P kept in LDS as the FULL symmetric matrix, row t at s_P + NN t (the packed upper triangle
+    // otherwise): every row read -- the K build, P v in the residual checks and the polish, the row after the
+    // penalties -- is NN / 2 contiguous ds_read_b128 from one base address instead of NN scattered reads with
+    // per-entry address selects, and the scaled rows are written back whole.  The same values in the same
+    // arithmetic (each lane reads exactly the entries it read from the packed triangle, which every writer keeps
+    // symmetric bit for bit), so the results do not change.  Costs (NN - 1) NN / 2 doubles more LDS: 6.2 KB at
+    // capacity 40 -- the fused 2-wave instance's image grows to 19.0 KB, still 8 workgroups per CU; the 3-wave
+    // instance's 12.8 KB budget, the per-step kernels' staging tail and capacity 64 keep the packed form.
+    constexpr bool FULLP = TGMPC_FULLP && CMP && !LEAN && NN <= 40;
+    constexpr int NP = FULLP ? NN * NN : NP0;
     __shared__ double s_pref0[(CMP || L2W) ? 2 : 3 * (NM + 1)];
     __shared__ double s_vref0[(CMP || L2W) ? 2 : NM + 1];
     __shared__ double s_x0[6], s_up[2];
@@ -683,7 +696,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #pragma unroll
                     for (int reg = 0; reg < 4; ++reg) {
                         const int i = 16 * ib + ((t >> 4) & 3) + 4 * reg, j = 16 * jb + mc;
-                        if (i <= j && j < NN) s_P[i * NN - (i * (i - 1)) / 2 + (j - i)] = acc[ti][reg];
+                        if constexpr (FULLP) {
+                            if (i <= j && j < NN) {
+                                s_P[i * NN + j] = acc[ti][reg];
+                                s_P[j * NN + i] = acc[ti][reg];
+                            }
+                        } else {
+                            if (i <= j && j < NN) s_P[i * NN - (i * (i - 1)) / 2 + (j - i)] = acc[ti][reg];
+                        }
                     }
             __syncthreads();
         }
@@ -703,21 +723,34 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         // lower entry is the upper entry of another row with the same term bit for bit (Rs[1] = Rs[2],
         // Rds[1] = Rds[2]), so adding each entry once gives the rows the per-entry loop gave.
         if (own) {
-            const int rb0 = t * NN - (t * (t - 1)) / 2 - t;   // packed row t: P(t, j) at rb0 + j
+            // (FULLP: each upper entry's mirror gets the same sum -- the two were equal bit for bit)
+            const int rb0 = FULLP ? t * NN : t * NN - (t * (t - 1)) / 2 - t;   // row t: P(t, j) at rb0 + j (j >= t)
+            auto addp = [&](int j, double v) {
+                const double nv = s_P[rb0 + j] + v;
+                s_P[rb0 + j] = nv;
+                if constexpr (FULLP) s_P[j * NN + t] = nv;
+            };
             s_P[rb0 + t] = s_P[rb0 + t] + (2.0 * (ch ? Rs1 : Rs0) + 2.0 * (ch ? Rd1 : Rd0) * dmul);
             if (ch == 0) {
-                s_P[rb0 + t + 1] = s_P[rb0 + t + 1] + (2.0 * Rs1 + 2.0 * Rd1 * dmul);
-                if (t + 2 < n) s_P[rb0 + t + 2] = s_P[rb0 + t + 2] + -2.0 * Rd0;
-                if (t + 3 < n) s_P[rb0 + t + 3] = s_P[rb0 + t + 3] + -2.0 * Rd1;
+                addp(t + 1, 2.0 * Rs1 + 2.0 * Rd1 * dmul);
+                if (t + 2 < n) addp(t + 2, -2.0 * Rd0);
+                if (t + 3 < n) addp(t + 3, -2.0 * Rd1);
             } else {
-                if (t + 1 < n) s_P[rb0 + t + 1] = s_P[rb0 + t + 1] + -2.0 * Rd0;
-                if (t + 2 < n) s_P[rb0 + t + 2] = s_P[rb0 + t + 2] + -2.0 * Rd1;
+                if (t + 1 < n) addp(t + 1, -2.0 * Rd0);
+                if (t + 2 < n) addp(t + 2, -2.0 * Rd1);
             }
         }
         __syncthreads();
         const int tt = opaque_t();
+        if constexpr (FULLP) {
+            const int tr = tt < NN ? tt : NN - 1;
+            lds_load_all<NN>(s_P + tr * NN, Prow);
 #pragma unroll
-        for (int j = 0; j < NN; ++j) Prow[j] = own ? s_P[paddr(j, tt)] : 0.0;
+            for (int j = 0; j < NN; ++j) Prow[j] = own ? Prow[j] : 0.0;
+        } else {
+#pragma unroll
+            for (int j = 0; j < NN; ++j) Prow[j] = own ? s_P[paddr(j, tt)] : 0.0;
+        }
     } else if (own) {
 #pragma unroll
         for (int j = 0; j < NN; ++j) {
@@ -871,7 +904,16 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         };
         // scaled P to LDS (row stride PS)
         // packed upper triangle: P(i, j), i <= j, at i*NN - i(i-1)/2 + (j - i); rows >= n are zero
-        if (t < NN) {
+        if constexpr (FULLP) {
+            // the whole row (symmetric bit for bit: lane t's D_t D_j products equal lane j's), 16-byte stores
+            if (t < NN) {
+                double2* const w2 = reinterpret_cast<double2*>(__builtin_assume_aligned(s_P + t * NN, 16));
+#pragma unroll
+                for (int j = 0; j < NN; j += 2)
+                    w2[j / 2] = double2{own ? Prow[j] : ((j == t) ? 1.0 : 0.0),
+                                        own ? Prow[j + 1] : ((j + 1 == t) ? 1.0 : 0.0)};   // identity on padding rows
+            }
+        } else if (t < NN) {
             const int rt = t * NN - (t * (t - 1)) / 2 - t;
 #pragma unroll
             for (int j = 0; j < NN; ++j)
@@ -904,6 +946,22 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 for (int c0 = 0; c0 < NN; c0 += 8) {
 #pragma unroll
                     for (int jj = 0; jj < 8; ++jj) sa[jj] = fma(prow_entry(c0 + jj, tt, rt), vb[c0 + jj], sa[jj]);
+                }
+            } else if constexpr (FULLP) {
+                // the row and the broadcast in chunks of 8 (16-byte reads), same products in the same chains
+                const double2* pr2 = reinterpret_cast<const double2*>(
+                    __builtin_assume_aligned(s_P + (tt < NN ? tt : NN - 1) * NN, 16));
+                const double2* vb2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb, 16));
+#pragma unroll
+                for (int c0 = 0; c0 < NN; c0 += 8) {
+                    double2 pv[4], vv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) { pv[i] = pr2[c0 / 2 + i]; vv[i] = vb2[c0 / 2 + i]; }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        sa[(c0 + 2 * i) & 7] = fma(pv[i].x, vv[i].x, sa[(c0 + 2 * i) & 7]);
+                        sa[(c0 + 2 * i + 1) & 7] = fma(pv[i].y, vv[i].y, sa[(c0 + 2 * i + 1) & 7]);
+                    }
                 }
             } else {
 #pragma unroll
@@ -1130,7 +1188,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 // are restored.  Padding rows n..NN-1 hold the identity in s_P; lanes >= NN hold exact zero rows
                 // (the receivers of the one-wave sweep below).
                 const int tt = opaque_t();
-                const int pdg = paddr(tt, tt), psp = paddr(tt + 2, tt);
+                const int pdg = FULLP ? tt * NN + tt : paddr(tt, tt), psp = FULLP ? tt * NN + tt + 2 : paddr(tt + 2, tt);
+                const int psm = (tt + 2) * NN + tt;   // FULLP: the mirror of (t, t + 2)
                 const bool has_sp = own && (t + 2 < n);
                 double o_dg = 0.0, o_sp = 0.0;
                 if (own) {
@@ -1139,6 +1198,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     if (has_sp) {
                         o_sp = s_P[psp];
                         s_P[psp] = o_sp + dp;
+                        if constexpr (FULLP) s_P[psm] = o_sp + dp;
                     }
                 }
                 __syncthreads();
@@ -1148,6 +1208,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const int rr = r >= 0 ? r : 0;
 #pragma unroll
                     for (int j = 0; j < NN; ++j) Krow[j] = (r >= 0) ? s_P[paddr(j, rr)] : 0.0;
+                } else if constexpr (FULLP) {
+                    // (lanes >= NN: exact zero rows, the one-wave sweep's receivers)
+                    lds_load_all<NN>(s_P + (tt < NN ? tt : NN - 1) * NN, Krow);
+                    if (t >= NN) {
+#pragma unroll
+                        for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
+                    }
                 } else if (WAVES > 1 || t < NN) {
 #pragma unroll
                     for (int j = 0; j < NN; ++j) Krow[j] = (WAVES == 1 || t < NN) ? s_P[paddr(j, tt)] : 0.0;
@@ -1158,7 +1225,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 __syncthreads();
                 if (own) {
                     s_P[pdg] = o_dg;
-                    if (has_sp) s_P[psp] = o_sp;
+                    if (has_sp) {
+                        s_P[psp] = o_sp;
+                        if constexpr (FULLP) s_P[psm] = o_sp;
+                    }
                 }
             }
             // ---- sweep: Krow <- row t of K^{-1} (symmetric sweep operator, NN pivots) ----
