@@ -5,8 +5,8 @@
 // (:73-109) evaluate atan2 -> atan -> sin per tire and sin / cos(phi) per stage; in the fused closed loop that
 // chain is ~20 % of a work item's instructions.  These routines:
 //   * fm_sincos: x = n pi/2 + r with n = rint(x 2/pi) and r = fma(-n, PIO2_HI, x) (exact for |n| < 2^20: both
-//     terms are multiples of 2^-53 and |r| <= pi/4) minus n PIO2_MID; the kernel polynomials of FreeBSD's
-//     k_sin.c / k_cos.c (|r| <= pi/4, < 1 ulp), quadrant by n mod 4.  |x| >= 2^20 pi/2 or non-finite: the device
+//     terms are multiples of 2^-53 and |r| <= pi/4) minus n PIO2_MID, its rounding kept as a tail; the kernel
+//     polynomials of FreeBSD's k_sin.c / k_cos.c with that tail (|r| <= pi/4, < 1 ulp), quadrant by n mod 4.  |x| >= 2^20 pi/2 or non-finite: the device
 //     library's sincos for that lane.
 //   * fm_atan: |x| reduced to |r| <= 7/16 in three regions -- r = |x| (|x| <= 7/16); r = (|x| - 1) / (|x| + 1),
 //     offset pi/4 (<= 39/16); r = -1 / |x|, offset pi/2 -- with ONE division (v_rcp_f64 + 2 Newton steps + one
@@ -14,8 +14,8 @@
 //     offset sum.
 //   * fm_atan2: the same core on the pair (|y|, |x|) (no rounded quotient y / x first), then the quadrant;
 //     non-finite or (0, 0) arguments take the device library's atan2 for that lane.
-// Accuracy against 80-bit references (tools/fastmath_check.cpp, 2e7 points per range): <= 1 ulp for sincos
-// (observed max 0.9), <= 1.5 ulp for atan / atan2.  The reference path's own functions are numpy's (glibc):
+// Accuracy against 80-bit references (tools/microbench/fastmath_check.hip, 4 M points per range on the GPU): see
+// DESIGN.md (the device library's own routines: 0.8 ulp sin / cos, 1.5 atan, 1.6 atan2).  The reference path's own functions are numpy's (glibc):
 // the physics fixtures are checked at 1e-12 relative and the difference quotients at 1e-8 (tests/).
 // Every caller in the MPC path (fused and per-step kernels, the physics entry points, the window kernels) uses
 // these, so the fused closed loop and the per-step launches stay bit-identical.
@@ -42,19 +42,21 @@ constexpr double PIO4_HI = 7.85398163397448278999e-01, PIO4_LO = 3.0616169978683
 constexpr double PIO2_HI = 1.57079632679489655800e+00, PIO2_LO = 6.12323399573676603587e-17;
 constexpr double PI_HI = 3.1415926535897931160e+00, PI_LO = 1.2246467991473531772e-16;
 constexpr double TWO_OVER_PI = 6.36619772367581382433e-01;
+constexpr double PIO2_MID = 6.123233995736766035868820147291818e-17;   // pi/2 - PIO2_HI
 constexpr double SC_LIMIT = 1647099.3291652855;   // 2^20 pi / 2
 
 __device__ __forceinline__ double flip(double v, bool neg) {   // v or -v (sign bit)
     return neg ? -v : v;
 }
-// sin(r), cos(r) for |r| <= pi/4 (k_sin.c / k_cos.c with a zero tail)
-__device__ __forceinline__ void kernel_sincos(double r, double& s, double& c) {
+// sin(r + y), cos(r + y) for |r| <= pi/4, y the reduction's tail (k_sin.c / k_cos.c)
+__device__ __forceinline__ void kernel_sincos(double r, double y, double& s, double& c) {
     const double z = r * r, w = z * z;
     const double rs = fma(z, fma(z, S4, S3), S2) + z * w * fma(z, S6, S5);
-    s = fma(z * r, fma(z, rs, S1), r);
+    const double v = z * r;
+    s = r - ((z * (0.5 * y - v * rs) - y) - v * S1);
     const double rc = z * fma(z, fma(z, C3, C2), C1) + w * w * fma(z, fma(z, C6, C5), C4);
     const double hz = 0.5 * z, wc = 1.0 - hz;
-    c = wc + (((1.0 - wc) - hz) + z * rc);
+    c = wc + (((1.0 - wc) - hz) + (z * rc - r * y));
 }
 // atan(num / den) for a reduced pair with |num / den| <= 7/16 (den >= 1), plus offset (hi, lo):
 // off_hi - ((r s - off_lo) - r) as s_atan.c
@@ -90,9 +92,11 @@ __device__ __forceinline__ void fm_sincos(double x, double* sp, double* cp) {
         return;
     }
     const double n = rint(x * fmk::TWO_OVER_PI);
-    const double r = fma(-n, 6.123233995736766035868820147291818e-17, fma(-n, fmk::PIO2_HI, x));
+    const double r1 = fma(-n, fmk::PIO2_HI, x);                 // exact (see above)
+    const double r = fma(-n, fmk::PIO2_MID, r1);
+    const double y = fma(-n, fmk::PIO2_MID, r1 - r);            // the rounding of r (the pi/2 tail past MID is < 1e-32 n)
     double s, c;
-    fmk::kernel_sincos(r, s, c);
+    fmk::kernel_sincos(r, y, s, c);
     const int q = (int)n & 3;
     const bool swap = q & 1;
     *sp = fmk::flip(swap ? c : s, q & 2);

@@ -102,7 +102,7 @@ __device__ inline void path_eval(const PathArgs& pa, int b, double x, double& y,
     } else if (kind == 1) {
         double a = c[1] * x + c[2];
         double s, co;
-        sincos(a, &s, &co);
+        pm_sincos(a, &s, &co);
         y = c[0] * s + c[3];
         dy = c[0] * c[1] * co;
     } else {

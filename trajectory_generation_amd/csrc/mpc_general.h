@@ -441,7 +441,8 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
         double cst = 0.0;   // thread 0's copy is the one used
         for (int k = 0; k <= N; ++k) {
             const double Xr = pref[k * 3 + 0], Yr = pref[k * 3 + 1], Pr = pref[k * 3 + 2];
-            const double s = sin(Pr), co = cos(Pr);
+            double s, co;
+            pm_sincos(Pr, &s, &co);
             const double* xk = w.xh + 6 * k;
             double e3[3];
             e3[0] = s * (xk[0] - Xr) - co * (xk[1] - Yr);

@@ -30,12 +30,12 @@ __device__ __forceinline__ void rollout_f(const VP& p, const double* x, double d
     const double avx = fabs(vx);
     const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
     const double vx_eff = np_sign(vx) * mx;
-    const double alpha_f = clampd(-atan2(omega * p.lf + vy, vx_eff) + delta, -p.maxAlpha, p.maxAlpha);
-    const double alpha_r = clampd(atan2(omega * p.lr - vy, vx_eff), -p.maxAlpha, p.maxAlpha);
+    const double alpha_f = clampd(-pm_atan2(omega * p.lf + vy, vx_eff) + delta, -p.maxAlpha, p.maxAlpha);
+    const double alpha_r = clampd(pm_atan2(omega * p.lr - vy, vx_eff), -p.maxAlpha, p.maxAlpha);
     double sf, cf, sr, cr, sphi, cphi;
-    sincos(p.Cf * atan(p.Bf * alpha_f), &sf, &cf);
-    sincos(p.Cr * atan(p.Br * alpha_r), &sr, &cr);
-    sincos(phi, &sphi, &cphi);
+    pm_sincos(p.Cf * pm_atan(p.Bf * alpha_f), &sf, &cf);
+    pm_sincos(p.Cr * pm_atan(p.Br * alpha_r), &sr, &cr);
+    pm_sincos(phi, &sphi, &cphi);
     const double Fy_f = p.Df * sf, Fy_r = p.Dr * sr;
     const double Frx = (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
     xd[0] = vx * cphi - vy * sphi;
@@ -59,7 +59,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(const KArgs a) {
     for (int i = 0; i < 6; ++i) x[i] = xs[i];
     const double u0 = us[0], u1 = us[1];
     double sd, cd;
-    sincos(u1, &sd, &cd);
+    pm_sincos(u1, &sd, &cd);
     double* rec = a.wsXF + (size_t)b * N * 12;
     for (int k = 0; k < N; ++k) {
         rollout_f(p, x, u0, u1, sd, cd, f);
@@ -80,24 +80,24 @@ __device__ __forceinline__ Tire tire_angles(const VP& p, double vx, double vy, d
     const double avx = fabs(vx);
     const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
     r.vx_eff = np_sign(vx) * mx;
-    r.atf = atan2(omega * p.lf + vy, r.vx_eff);
-    r.atr = atan2(omega * p.lr - vy, r.vx_eff);
+    r.atf = pm_atan2(omega * p.lf + vy, r.vx_eff);
+    r.atr = pm_atan2(omega * p.lr - vy, r.vx_eff);
     return r;
 }
 // The Pacejka sine as the sine of sincos: the lane-parallel chains of block_linearize evaluate
 // sincos for every lane (the phi lanes need the cosine), so the per-step kernels take the same value.
 __device__ __forceinline__ double tire_sin(double z) {
     double s, c;
-    sincos(z, &s, &c);
+    pm_sincos(z, &s, &c);
     return s;
 }
 __device__ __forceinline__ double front_force(const VP& p, double atf, double delta) {
     const double alpha_f = clampd(-atf + delta, -p.maxAlpha, p.maxAlpha);
-    return p.Df * tire_sin(p.Cf * atan(p.Bf * alpha_f));
+    return p.Df * tire_sin(p.Cf * pm_atan(p.Bf * alpha_f));
 }
 __device__ __forceinline__ double rear_force(const VP& p, double atr) {
     const double alpha_r = clampd(atr, -p.maxAlpha, p.maxAlpha);
-    return p.Dr * tire_sin(p.Cr * atan(p.Br * alpha_r));
+    return p.Dr * tire_sin(p.Cr * pm_atan(p.Br * alpha_r));
 }
 __device__ __forceinline__ double long_force(const VP& p, double vx, double d) {
     return (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
@@ -127,8 +127,8 @@ __device__ __forceinline__ void state_column(const VP& p, const double* xb, doub
     const double eps = 1e-5;
     const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
     double sphi, cphi, sd, cd;
-    sincos(phi, &sphi, &cphi);
-    sincos(de, &sd, &cd);
+    pm_sincos(phi, &sphi, &cphi);
+    pm_sincos(de, &sd, &cd);
     double fp[6], fm[6];
     f_full(p, grp == 0 ? xb[3] + eps : vx, grp == 1 ? xb[4] + eps : vy, grp == 2 ? xb[5] + eps : om, sphi, cphi, d,
            de, sd, cd, fp);
@@ -143,15 +143,15 @@ __device__ __forceinline__ void cheap_columns(const VP& p, const double* xb, dou
     const double eps = 1e-5;
     const double phi = xb[2] + 0.0, vx = xb[3] + 0.0, vy = xb[4] + 0.0, om = xb[5] + 0.0;
     double sphi, cphi, sd, cd;
-    sincos(phi, &sphi, &cphi);
-    sincos(de, &sd, &cd);
+    pm_sincos(phi, &sphi, &cphi);
+    pm_sincos(de, &sd, &cd);
     double fp[6], fm[6];
     const Tire t0 = tire_angles(p, vx, vy, om);
     const double Ff0 = front_force(p, t0.atf, de), Fr0 = rear_force(p, t0.atr), Fx0 = long_force(p, vx, d);
     {   // phi: only sin/cos(phi) change
         double sp, cp, sm, cm;
-        sincos(xb[2] + eps, &sp, &cp);
-        sincos(xb[2] - eps, &sm, &cm);
+        pm_sincos(xb[2] + eps, &sp, &cp);
+        pm_sincos(xb[2] - eps, &sm, &cm);
         f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
         f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
         for (int r = 0; r < 6; ++r) Jphi[r] = (fp[r] - fm[r]) / (2.0 * eps);
@@ -163,8 +163,8 @@ __device__ __forceinline__ void cheap_columns(const VP& p, const double* xb, dou
     }
     {   // delta: front force and sin/cos(delta) change
         double sp, cp, sm, cm;
-        sincos(de + eps, &sp, &cp);
-        sincos(de - eps, &sm, &cm);
+        pm_sincos(de + eps, &sp, &cp);
+        pm_sincos(de - eps, &sm, &cm);
         f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
         f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
         for (int r = 0; r < 6; ++r) Jde[r] = (fp[r] - fm[r]) / (2.0 * eps);
@@ -252,11 +252,11 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 // columns of stage k need the same chain at perturbed copies of x_k, known as soon as x_k is: lanes
 // 3 .. 21 run those evaluations IN THE SAME instruction stream as the rollout lanes (the stage's
 // latency does not change; round 1 ran them as a separate 29 k-cycle pass).  Lane roles, stage k:
-//   0 / 1 / 2   rollout: front tire, rear tire, sincos(phi) at x_k (raw, rollout_kernel's form)
+//   0 / 1 / 2   rollout: front tire, rear tire, pm_sincos(phi) at x_k (raw, rollout_kernel's form)
 //   3 / 4       base front / rear tire at x_k + 0.0 (cheap_columns' t0)
 //   5 .. 16     4 lanes per state column (vx, vy, omega): (+eps front, +eps rear, -eps front, -eps rear)
 //   17 / 18     front tire at delta +- eps (the delta column)
-//   19 / 20     sincos(phi +- eps) (the phi column);   21   sincos(phi + 0.0)
+//   19 / 20     pm_sincos(phi +- eps) (the phi column);   21   pm_sincos(phi + 0.0)
 // Their sines go to tj[k][lane], the cosines of lanes 19 .. 21 to tj[k][0 .. 2].  An assembly pass (one
 // stage per lane) then forms f at each perturbed point with f_parts and the difference quotients:
 // the values state_column / cheap_columns compute (jac_kernel), bit for bit.
@@ -279,7 +279,7 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
         for (int i = 0; i < 6; ++i) x[i] = xs[i];
         const double u0 = us[0], u1 = us[1];
         double sd, cd;
-        sincos(u1, &sd, &cd);
+        pm_sincos(u1, &sd, &cd);
         // this lane's role (see above): tire chain or sincos, which tire, which input it perturbs
         const bool roll = t < 3;
         const bool tire = (t < 2) || (t >= 3 && t <= 18);
@@ -298,11 +298,11 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
             const double avx = fabs(vxl);
             const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
             const double vx_eff = np_sign(vxl) * mx;
-            const double at = atan2(fr ? oml * p.lf + vyl : oml * p.lr - vyl, vx_eff);
+            const double at = pm_atan2(fr ? oml * p.lf + vyl : oml * p.lr - vyl, vx_eff);
             const double alpha = clampd(fr ? -at + dlt : at, -p.maxAlpha, p.maxAlpha);
-            const double z = tire ? Ct * atan(Bt * alpha) : (t == 2 ? phi : phi + pz);
+            const double z = tire ? Ct * pm_atan(Bt * alpha) : (t == 2 ? phi : phi + pz);
             double sz, cz;
-            sincos(z, &sz, &cz);
+            pm_sincos(z, &sz, &cz);
             if (t >= 3 && t <= 21) tj[LREC * k + t] = sz;
             if (t >= 19 && t <= 21) tj[LREC * k + t - 19] = cz;
             const double Fy_f = p.Df * readlane_d(sz, 0), Fy_r = p.Dr * readlane_d(sz, 1);
@@ -330,9 +330,9 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
     // assembly: one stage per lane -- f at every perturbed point from the stored sines (f_parts, the
     // reference's difference quotients), A = I + Ts Jx, B = Ts Ju, g = x + Ts f - A x - B u
     double sd, cd, sdp, cdp, sdm, cdm;
-    sincos(de, &sd, &cd);
-    sincos(de + eps, &sdp, &cdp);
-    sincos(de - eps, &sdm, &cdm);
+    pm_sincos(de, &sd, &cd);
+    pm_sincos(de + eps, &sdp, &cdp);
+    pm_sincos(de - eps, &sdm, &cdm);
     for (int k = t; k < N; k += NT) {
         const double* T = tj + LREC * k;
         double xb[6], fk[6];

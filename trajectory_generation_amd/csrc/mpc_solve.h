@@ -443,7 +443,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double y, dy;
             path_eval(a.path, b, s_pref[3 * k], y, dy);
             s_pref[3 * k + 1] = y;
-            s_pref[3 * k + 2] = atan(dy);
+            s_pref[3 * k + 2] = pm_atan(dy);
         }
         __syncthreads();
     }
@@ -498,7 +498,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // sin / cos of phi*_k for every stage (lane-parallel)
     for (int k = t; k <= N; k += NT) {
         double sk, ck;
-        sincos(s_pref[3 * k + 2], &sk, &ck);
+        pm_sincos(s_pref[3 * k + 2], &sk, &ck);
         s_sc[2 * k] = sk;
         s_sc[2 * k + 1] = ck;
     }

@@ -6,8 +6,45 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/trajmpc.h"
+#include "fastmath.h"
+
+#ifndef TGMPC_FASTMATH
+// 1: the MPC path's sincos / atan / atan2 from fastmath.h.  Measured slower (rollout 50.6 k -> 55.4 k cycles per
+// item, 12.36 -> 11.99 M steps/s at the driver's command; the per-lane fallback branches and region selects cost
+// more than the shorter polynomials save), so the device library's routines stay the default.
+#define TGMPC_FASTMATH 0
+#endif
 
 namespace tgmpc {
+
+// The transcendentals of the MPC path: every kernel (fused closed loop, per-step launches, physics and window
+// entry points) calls these, so all of them evaluate f, the slip angles and the window identically.
+__device__ __forceinline__ void pm_sincos(double x, double* s, double* c) {
+#if TGMPC_FASTMATH
+    fm_sincos(x, s, c);
+#else
+    sincos(x, s, c);
+#endif
+}
+__device__ __forceinline__ double pm_sin(double x) {
+    double s, c;
+    pm_sincos(x, &s, &c);
+    return s;
+}
+__device__ __forceinline__ double pm_atan(double x) {
+#if TGMPC_FASTMATH
+    return fm_atan(x);
+#else
+    return atan(x);
+#endif
+}
+__device__ __forceinline__ double pm_atan2(double y, double x) {
+#if TGMPC_FASTMATH
+    return fm_atan2(y, x);
+#else
+    return atan2(y, x);
+#endif
+}
 
 typedef traj_vehicle_params VP;
 
@@ -28,12 +65,12 @@ __device__ __forceinline__ void tire_forces(const VP& p, double vx, double vy, d
     double avx = fabs(vx);
     double mx = (p.vx_zero > avx) ? p.vx_zero : avx;  // python max(abs(vx), vx_zero)
     double vx_eff = np_sign(vx) * mx;
-    double alpha_f = -atan2(omega * p.lf + vy, vx_eff) + delta;
-    double alpha_r = atan2(omega * p.lr - vy, vx_eff);
+    double alpha_f = -pm_atan2(omega * p.lf + vy, vx_eff) + delta;
+    double alpha_r = pm_atan2(omega * p.lr - vy, vx_eff);
     alpha_f = clampd(alpha_f, -p.maxAlpha, p.maxAlpha);
     alpha_r = clampd(alpha_r, -p.maxAlpha, p.maxAlpha);
-    Fy_f = p.Df * sin(p.Cf * atan(p.Bf * alpha_f));
-    Fy_r = p.Dr * sin(p.Cr * atan(p.Br * alpha_r));
+    Fy_f = p.Df * pm_sin(p.Cf * pm_atan(p.Bf * alpha_f));
+    Fy_r = p.Dr * pm_sin(p.Cr * pm_atan(p.Br * alpha_r));
     Frx = (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
 }
 
@@ -44,7 +81,7 @@ __device__ __forceinline__ void f_cont_sc(const VP& p, const double* x, double d
     double Fy_f, Fy_r, Frx;
     tire_forces(p, vx, vy, omega, d, delta, Fy_f, Fy_r, Frx);
     double sphi, cphi;
-    sincos(phi, &sphi, &cphi);
+    pm_sincos(phi, &sphi, &cphi);
     xd[0] = vx * cphi - vy * sphi;
     xd[1] = vx * sphi + vy * cphi;
     xd[2] = omega;
@@ -55,14 +92,14 @@ __device__ __forceinline__ void f_cont_sc(const VP& p, const double* x, double d
 
 __device__ __forceinline__ void f_cont(const VP& p, const double* x, const double* u, double* xd) {
     double sd, cd;
-    sincos(u[1], &sd, &cd);
+    pm_sincos(u[1], &sd, &cd);
     f_cont_sc(p, x, u[0], u[1], sd, cd, xd);
 }
 
 // mpc_6stati.py:111-117
 __device__ __forceinline__ double lateral_error(double X, double Y, double Xr, double Yr, double phir) {
     double s, c;
-    sincos(phir, &s, &c);
+    pm_sincos(phir, &s, &c);
     return s * (X - Xr) - c * (Y - Yr);
 }
 

@@ -125,7 +125,7 @@ __global__ void ref_window_kernel(PathArgs pa, int B, int N, double Ts, const do
         double* o = pref + ((size_t)(N + 1) * b + k) * 3;
         o[0] = xs;
         o[1] = y;
-        o[2] = atan(dy);
+        o[2] = pm_atan(dy);
     }
 }
 
