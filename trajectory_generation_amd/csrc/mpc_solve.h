@@ -148,7 +148,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // symmetric bit for bit), so the results do not change.  Costs (NN - 1) NN / 2 doubles more LDS: 6.2 KB at
     // capacity 40 -- the fused 2-wave instance's image grows to 19.0 KB, still 8 workgroups per CU; the 3-wave
     // instance's 12.8 KB budget, the per-step kernels' staging tail and capacity 64 keep the packed form.
-    constexpr bool FULLP = TGMPC_FULLP && CMP && !LEAN && NN <= 40;
+    // (and the fused capacity-80 instance at one wave per SIMD: 73 KB per workgroup, 2 per CU as before)
+    constexpr bool FULLP = TGMPC_FULLP && !LEAN && ((CMP && NN <= 40) || (FUSED && WAVES == 2 && !L2W));
     constexpr int NP = FULLP ? NN * NN : NP0;
     __shared__ double s_pref0[(CMP || L2W) ? 2 : 3 * (NM + 1)];
     __shared__ double s_vref0[(CMP || L2W) ? 2 : NM + 1];
@@ -662,6 +663,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const double2* b2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(buf, 16));
 #pragma unroll
                     for (int c0 = 0; c0 < NN; c0 += 8) {
+                        if (TGMPC_COND_SPARSE && c0 >= 2 * k + 2) continue;   // F_k's zero columns (see below)
                         double2 f0[4], f1[4], f2[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
@@ -678,9 +680,16 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                         __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
                     }
                 } else {
+                    // F_k's columns >= 2 (k + 1) are exact zeros (the inputs of later stages do not move x_{k+1}):
+                    // their three fmas add exact zeros to the row and are skipped, 8 columns at a time (a uniform
+                    // branch; bit-identical -- about half of the stage loop's fmas at N = 40)
 #pragma unroll
-                    for (int j = 0; j < NN; ++j)
-                        Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
+                    for (int c0 = 0; c0 < NN; c0 += 8) {
+                        if (TGMPC_COND_SPARSE && c0 >= 2 * k + 2) continue;
+#pragma unroll
+                        for (int j = c0; j < c0 + 8; ++j)
+                            Prow[j] = fma(F0, buf[j], fma(F1, buf[NN + j], fma(F2, buf[2 * NN + j], Prow[j])));
+                    }
                 }
             }
         }
@@ -937,7 +946,23 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double* vb = bcast(v);
             const int tt = opaque_t();
             double sa[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-            if constexpr (LEAN || (WAVES > 1 && TGMPC_PMUL80) || (CMP && TGMPC_PMUL_W2)) {
+            if constexpr (FULLP && WAVES > 1) {
+                // contiguous row, ROLLED over blocks of 8 (see below); same products in the same chains
+                const double2* pr2 = reinterpret_cast<const double2*>(
+                    __builtin_assume_aligned(s_P + (tt < NN ? tt : NN - 1) * NN, 16));
+                const double2* vb2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb, 16));
+#pragma nounroll
+                for (int c0 = 0; c0 < NN; c0 += 8) {
+                    double2 pv[4], vv[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) { pv[i] = pr2[c0 / 2 + i]; vv[i] = vb2[c0 / 2 + i]; }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        sa[2 * i] = fma(pv[i].x, vv[i].x, sa[2 * i]);
+                        sa[2 * i + 1] = fma(pv[i].y, vv[i].y, sa[2 * i + 1]);
+                    }
+                }
+            } else if constexpr (LEAN || (WAVES > 1 && TGMPC_PMUL80) || (CMP && TGMPC_PMUL_W2)) {
                 // a ROLLED loop over blocks of 8 (the row of K^-1 stays live across this: fully unrolled, the
                 // scheduler issues all 80 reads at once and the ADMM loop around it spills); same sums, same order
                 static_assert(NN % 8 == 0, "Pmul blocks");
@@ -1207,7 +1232,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const int r = tt - SP2;
                     const int rr = r >= 0 ? r : 0;
 #pragma unroll
-                    for (int j = 0; j < NN; ++j) Krow[j] = (r >= 0) ? s_P[paddr(j, rr)] : 0.0;
+                    for (int j = 0; j < NN; ++j) Krow[j] = (r >= 0) ? s_P[FULLP ? rr * NN + j : paddr(j, rr)] : 0.0;
                 } else if constexpr (FULLP) {
                     // (lanes >= NN: exact zero rows, the one-wave sweep's receivers)
                     lds_load_all<NN>(s_P + (tt < NN ? tt : NN - 1) * NN, Krow);
