@@ -256,6 +256,9 @@ int traj_debug_queue_lead(int steps, int per_mille);
  * Results do not depend on it (the instances are bit-identical).  For experiments and tests. */
 int traj_debug_fused_waves(int waves);
 int traj_debug_kernel_times(double* ms, int* n_steps);
+/* traj_mpc_step_batch's linearization: 1 (default) inside the solve launch (one launch per call), 0 = the
+ * rollout and Jacobian kernels before it.  Results do not depend on it (bit-identical).  For tests. */
+int traj_debug_step_linearize(int in_kernel);
 
 #ifdef __cplusplus
 }

@@ -556,6 +556,26 @@ def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
     assert np.array_equal(d["u_cmd"].cpu().numpy(), g["u_cmd"])
 
 
+@pytest.mark.parametrize("N,Ts", [(8, 0.05), (20, 0.05), (20, 0.02), (30, 0.05), (40, 0.05)])
+def test_step_in_kernel_linearization_bit_identical(gpu, N, Ts):
+    """traj_mpc_step_batch runs the linearization inside the solve launch (one launch per call, block_linearize's
+    stage records copied to the workspace for X_opt); it equals the rollout_kernel + jac_kernel + solve sequence bit
+    for bit in every output, at every kernel capacity (16, 40, 64, 80)."""
+    from trajectory_generation_amd import _lib
+    x0, up, pr, vr = random_instances(23, 48, N, Ts)
+    cfg = TB.config_struct(N=N, Ts=Ts)
+    outs = {}
+    try:
+        for mode in (1, 0):
+            _lib.check(_lib.lib().traj_debug_step_linearize(mode), "traj_debug_step_linearize")
+            outs[mode] = {k: v.cpu() for k, v in TB.mpc_step_batch(x0, up, pr, vr, cfg).items()}
+    finally:
+        _lib.lib().traj_debug_step_linearize(1)
+    for k in outs[0]:
+        a, b = outs[1][k], outs[0][k]
+        assert bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) if a.is_floating_point() else torch.equal(a, b), k
+
+
 def _lib_status(code):
     from trajectory_generation_amd._lib import STATUS_STRINGS
     return STATUS_STRINGS[int(code)]

@@ -16,7 +16,8 @@ int launch_fused_w3_40(const KArgs& a, hipStream_t st);   // mpc_inst_w3.hip
 #endif
 
 // mode 0: MPC step, 1: QP only (A/B/g given), 2: closed-loop step (the linearization launches are
-// issued by the caller, trajmpc.hip), 3: fused closed loop of a.nsteps steps (linearization inside)
+// issued by the caller, trajmpc.hip), 3: fused closed loop of a.nsteps steps (linearization inside),
+// 4: MPC step with the linearization inside (one launch; the records go to the workspace's A/B/g)
 int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
     constexpr int NN = TGMPC_NN;
     dim3 grid(a.B), sblock(((NN + 63) / 64) * 64);
@@ -33,6 +34,7 @@ int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
         return launch_fused<NN, 2>(a, st);
     }
     else if (mode == 2) hipLaunchKernelGGL((solve_kernel<NN, true>), grid, sblock, 0, st, a);
+    else if (mode == 4) hipLaunchKernelGGL((solve_kernel<NN, false, false, true, 2, true>), grid, sblock, 0, st, a);
     else hipLaunchKernelGGL((solve_kernel<NN, false>), grid, sblock, 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -118,7 +118,10 @@ __device__ __forceinline__ double ld_coh(const double* p) {
 // DIAG = false instance unless a diagnostic buffer is set (their counters cost registers in every phase)
 // WPS: waves per SIMD the register allocation is held to (fused one-wave kernels: 2, or 3 -- 168 VGPRs, the
 // compact LDS image; mpc_inst_w3.hip).
-template <int NN, bool CLOSED, bool FUSED = false, bool DIAG = true, int WPS = 2>
+// INLIN: the linearization runs in the workgroup (block_linearize, stage records in LDS) -- the fused closed loop,
+// and the step entry point (traj_mpc_step_batch: one launch per call instead of rollout + Jacobian + solve; the
+// records are copied to the workspace's A/B/g for X_opt).  Same values as rollout_kernel + jac_kernel.
+template <int NN, bool CLOSED, bool FUSED = false, bool DIAG = true, int WPS = 2, bool INLIN = FUSED>
 // (capacity 64: the row of K^-1 and its broadcast vector alone are 256 VGPRs -- one wave per SIMD; capacity 80,
 // two waves per instance: one wave per SIMD, or, fused with WPS = 2, two -- the lean two-wave instance below)
 __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_per_eu(
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // (L2W: the window -- X*, Y*, phi*, vref, sin / cos(phi*) -- after the stage records, read up to the condensing)
     constexpr int NLINW = NLIN + (L2W ? 6 * (NM + 1) : 0);
     constexpr int NBIG0 = (NP + NCOLD > NLINW) ? NP + NCOLD : NLINW;
-    constexpr int NDMA = FUSED ? 0 : 2 * NT * ((27 * NM + NT - 1) / NT);   // the LDS-DMA staging tail (below)
+    constexpr int NDMA = INLIN ? 0 : 2 * NT * ((27 * NM + NT - 1) / NT);   // the LDS-DMA staging tail (below)
     constexpr int NBIG = NBIG0 > NDMA ? NBIG0 : NDMA;
     __shared__ __attribute__((aligned(16))) double s_big[NBIG];
     double* const s_P = s_big;
@@ -464,9 +467,22 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     stamp(2, __builtin_amdgcn_s_memrealtime());   // 100 MHz wall clock (comparable across XCDs)
     // ---- 3. condensed QP (:180-250) --------------------------------------------------
     // A_k, B_k, g_k staged in LDS (coalesced copy); rows are then read as uniform broadcasts
-    if constexpr (FUSED) {
+    if constexpr (INLIN) {
         // A_k, B_k, g_k as stage records (LREC doubles each) in s_big
         block_linearize<NT>(t, p, N, Ts, s_x0, s_up, s_big, dbg ? dbg + (size_t)b * 32 : nullptr);
+        if constexpr (!FUSED) {
+            // the step entry point reports X_opt by the linear model (read back from A/B/g at the end)
+            double* const wA = const_cast<double*>(gA);
+            double* const wB = const_cast<double*>(gB);
+            double* const wg = const_cast<double*>(gg);
+            for (int i = t; i < 54 * N; i += NT) {
+                const int k = i / 54, e = i - 54 * k;
+                const double v = s_big[LREC * k + e];
+                if (e < 36) wA[36 * k + e] = v;
+                else if (e < 48) wB[12 * k + e - 36] = v;
+                else wg[6 * k + e - 48] = v;
+            }
+        }
     } else {
     if (((reinterpret_cast<uintptr_t>(gA) | reinterpret_cast<uintptr_t>(gB) | reinterpret_cast<uintptr_t>(gg)) & 15) == 0) {
         // LDS-DMA (global_load_lds_dwordx4): 16 bytes per lane straight into LDS, all chunks in flight
@@ -492,10 +508,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     }
     stamp(16, __builtin_amdgcn_s_memtime());
     // stage k's A_k at cA + RA k, B_k at cB + RB k, g_k at cg + RG k (fused: block_linearize's stage records)
-    constexpr int RA = FUSED ? LREC : 36, RB = FUSED ? LREC : 12, RG = FUSED ? LREC : 6;
+    constexpr int RA = INLIN ? LREC : 36, RB = INLIN ? LREC : 12, RG = INLIN ? LREC : 6;
     const double* const cA = s_big;
-    const double* const cB = s_big + (FUSED ? 36 : 36 * N);
-    const double* const cg = s_big + (FUSED ? 48 : 48 * N);
+    const double* const cB = s_big + (INLIN ? 36 : 36 * N);
+    const double* const cg = s_big + (INLIN ? 48 : 48 * N);
     // sin / cos of phi*_k for every stage (lane-parallel)
     for (int k = t; k <= N; k += NT) {
         double sk, ck;
