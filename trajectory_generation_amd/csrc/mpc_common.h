@@ -165,6 +165,26 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return r;
 }
 
+// max(a, b) and max(a, |b|) as ONE v_max_f64.  In the default IEEE mode fmax(a, fabs(b)) compiles to a
+// canonicalizing v_max_f64 of |b| with itself and then the max (two instructions per entry of a row norm); the
+// operands here are arithmetic results or copies of them, never signaling NaNs, and for those the single
+// instruction returns the same value (a quiet NaN operand yields the other one, as fmax does).
+__device__ __forceinline__ double vmax(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmax_abs(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmax_abs2(double a, double b) {   // max(|a|, |b|)
+    double r;
+    asm("v_max_f64 %0, |%1|, |%2|" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
 // Three-address fma (v_fma_f64 dst, a, b, c): keeps the compiler from turning a register-rotating
 // update into an in-place v_fmac plus register copies.
 __device__ __forceinline__ double fma3(double a, double b, double c) {
@@ -225,12 +245,12 @@ __device__ __forceinline__ void wave_max_dpp(double (&v)[V]) {
     for (int i = 0; i < V; ++i) {
         const bool nan = __ballot(v[i] != v[i]) != 0;
         double m = v[i];
-        m = fmax(m, dpp_d<0xB1>(m));
-        m = fmax(m, dpp_d<0x4E>(m));
-        m = fmax(m, dpp_d<0x141>(m));
-        m = fmax(m, dpp_d<0x140>(m));
-        m = fmax(m, dpp_d<0x142, 0xa>(m));
-        m = fmax(m, dpp_d<0x143, 0xc>(m));
+        m = vmax(m, dpp_d<0xB1>(m));
+        m = vmax(m, dpp_d<0x4E>(m));
+        m = vmax(m, dpp_d<0x141>(m));
+        m = vmax(m, dpp_d<0x140>(m));
+        m = vmax(m, dpp_d<0x142, 0xa>(m));
+        m = vmax(m, dpp_d<0x143, 0xc>(m));
         m = readlane_d(m, 63);
         v[i] = nan ? __builtin_nan("") : m;
     }

@@ -617,14 +617,16 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             // inputs enter through B_k
             // (branch-free: every lane forms A_k G, then selects -- no divergent exec juggling)
             {
+                // (a lane whose input has not entered yet holds G = +0, and A_k G started from +0 is +0 exactly: every
+                // lane but the two entering ones takes A_k G -- one select per row instead of two)
                 const bool fl = FREE_LANE && t == FL;
-                const bool prop = (own && (t < 2 * k)) || fl, enter = own && (kk == k);
+                const bool enter = own && (kk == k);
                 double Gn[6];
 #pragma unroll
                 for (int r = 0; r < 6; ++r) {
                     const double v = arow(Ak, r, G, fl ? cg[RG * k + r] : 0.0);
                     const double bv = cB[RB * k + 2 * r + ch];
-                    Gn[r] = prop ? v : (enter ? bv : G[r]);
+                    Gn[r] = enter ? bv : v;
                 }
 #pragma unroll
                 for (int r = 0; r < 6; ++r) G[r] = Gn[r];
@@ -837,18 +839,18 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         {
             double c4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < NN; ++j) c4[j & 3] = fmax(c4[j & 3], fabs(Prow[j]));
-            cn = fmax(fmax(c4[0], c4[1]), fmax(c4[2], c4[3]));
+            for (int j = 0; j < NN; ++j) c4[j & 3] = vmax_abs(c4[j & 3], Prow[j]);
+            cn = vmax(vmax(c4[0], c4[1]), vmax(c4[2], c4[3]));
         }
         for (int it = 0; it < c.scaling_iters; ++it) {
             double Er_up = exch(Er, +2);     // E of rate row t+2
             double D_dn = exch(D, -2);       // D of variable t-2
             double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
             const double pn = cs * cn;
-            double coln = fmax(pn, fmax(fabs(a_b), fmax(fabs(a_r), fabs(a_rp))));
+            double coln = vmax(pn, vmax_abs(vmax_abs2(a_b, a_r), a_rp));
             double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
             double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
-            double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
+            double Etr = 1.0 / sqrt(limit_scaling(vmax_abs2(a_r, a_rm)));
             // the broadcast D read in chunks of RCH, each chunk's reads in flight at once (CMP: 8, so that the
             // row of P and the chunk fit the 3-wave register budget; otherwise the whole vector)
             const double* dvb = bcast(Dt);
@@ -863,10 +865,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 for (int j = 0; j < RCH; ++j) {
                     const double v = Prow[c0 + j] * (Dt * Dv[j]);
                     Prow[c0 + j] = v;
-                    c4[(c0 + j) & 3] = fmax(c4[(c0 + j) & 3], fabs(v));
+                    c4[(c0 + j) & 3] = vmax_abs(c4[(c0 + j) & 3], v);
                 }
             }
-            cn = fmax(fmax(c4[0], c4[1]), fmax(c4[2], c4[3]));
+            cn = vmax(vmax(c4[0], c4[1]), vmax(c4[2], c4[3]));
             qi *= Dt;
             D *= Dt;
             Eb *= Etb;
@@ -1075,14 +1077,14 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             if (own) {
                 double dres = px + qi + aty;
                 const double Dinv = 1.0 / cold(C_D), Ebinv = 1.0 / cold(C_EB), Erinv = 1.0 / cold(C_ER);
-                v[0] = fmax(fabs(Ebinv * (axb - zb)), fabs(Erinv * (axr - zr)));   // prim res
-                v[1] = fmax(fmax(fabs(Ebinv * axb), fabs(Erinv * axr)), fmax(fabs(Ebinv * zb), fabs(Erinv * zr)));
+                v[0] = vmax_abs2(Ebinv * (axb - zb), Erinv * (axr - zr));   // prim res
+                v[1] = vmax(vmax_abs2(Ebinv * axb, Erinv * axr), vmax_abs2(Ebinv * zb, Erinv * zr));
                 v[2] = fabs(Dinv * dres) * csinv;
-                v[3] = fmax(fabs(Dinv * px) * csinv, fmax(fabs(Dinv * aty) * csinv, fabs(Dinv * qi) * csinv));
-                v[4] = fmax(fabs(axb - zb), fabs(axr - zr));
+                v[3] = vmax(fabs(Dinv * px) * csinv, vmax(fabs(Dinv * aty) * csinv, fabs(Dinv * qi) * csinv));
+                v[4] = vmax_abs2(axb - zb, axr - zr);
                 v[5] = fabs(dres);
-                v[6] = fmax(fmax(fabs(axb), fabs(axr)), fmax(fabs(zb), fabs(zr)));
-                v[7] = fmax(fabs(px), fmax(fabs(aty), fabs(qi)));
+                v[6] = vmax(vmax_abs2(axb, axr), vmax_abs2(zb, zr));
+                v[7] = vmax_abs(vmax_abs2(aty, qi), px);
             } else {
                 for (int i = 0; i < 8; ++i) v[i] = 0.0;
             }
@@ -1104,10 +1106,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 const double* src = s_F + (t >> 3) * NN + (t & 7) * PL;
                 double m = src[0];
 #pragma unroll
-                for (int k = 1; k < PL; ++k) m = fmax(m, src[k]);
-                m = fmax(m, dpp_d<0xB1>(m));    // lane ^ 1
-                m = fmax(m, dpp_d<0x4E>(m));    // lane ^ 2
-                m = fmax(m, dpp_d<0x141>(m));   // half-row mirror: quads of one 8-lane group
+                for (int k = 1; k < PL; ++k) m = vmax(m, src[k]);
+                m = vmax(m, dpp_d<0xB1>(m));    // lane ^ 1
+                m = vmax(m, dpp_d<0x4E>(m));    // lane ^ 2
+                m = vmax(m, dpp_d<0x141>(m));   // half-row mirror: quads of one 8-lane group
                 __syncthreads();
                 if ((t & 7) == 0) s_F[t >> 3] = m;
                 __syncthreads();
