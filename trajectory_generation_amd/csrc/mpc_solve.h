@@ -88,6 +88,9 @@
 #ifndef TGMPC_RECV2_L2W
 #define TGMPC_RECV2_L2W 1      // L2W: the receiver sweep as well (scratch 1,864 -> 396 B/lane; still opt-in)
 #endif
+#ifndef TGMPC_PSPAD
+#define TGMPC_PSPAD 2          // FULLP: row stride NN + TGMPC_PSPAD doubles (0: NN, the bank-conflicted stride)
+#endif
 #ifndef TGMPC_FULLP
 #define TGMPC_FULLP 1          // one-wave, non-lean instances: the scaled P in LDS as the full symmetric matrix (row-major)
 #endif
@@ -143,7 +146,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr bool L2W = FUSED && WAVES == 2 && WPS >= 2;
     constexpr bool LEAN = (CMP && WPS >= 3) || L2W;
     static_assert(!L2W || CLOSED, "the lean two-wave instance is the fused closed loop");
-    // FULLP: the scaled P kept in LDS as the FULL symmetric matrix, row t at s_P + NN t (the packed upper triangle
+    // FULLP: the scaled P kept in LDS as the FULL symmetric matrix, row t at s_P + PS t (the packed upper triangle
     // otherwise): every row read -- the K build, P v in the residual checks and the polish, the row after the
     // penalties -- is NN / 2 contiguous ds_read_b128 from one base address instead of NN scattered reads with
     // per-entry address selects, and the scaled rows are written back whole.  The same values in the same
@@ -153,7 +156,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // instance's 12.8 KB budget, the per-step kernels' staging tail and capacity 64 keep the packed form.
     // (and the fused capacity-80 instance at one wave per SIMD: 73 KB per workgroup, 2 per CU as before)
     constexpr bool FULLP = TGMPC_FULLP && !LEAN && ((CMP && NN <= 40) || (FUSED && WAVES == 2 && !L2W));
-    constexpr int NP = FULLP ? NN * NN : NP0;
+    // FULLP row stride PS = NN + 2 doubles (2 PS = 4 mod 8 dwords): a row-per-lane 16-byte read puts 16 consecutive
+    // lanes on 16 distinct 4-bank groups (stride NN = 40 maps every 4th lane to the same banks: 16-way conflicts)
+    constexpr int PS = FULLP ? NN + TGMPC_PSPAD : NN;
+    static_assert(!FULLP || TGMPC_PSPAD != 2 || (2 * PS) % 8 == 4, "conflict-free row stride");
+    constexpr int NP = FULLP ? NN * PS : NP0;
     __shared__ double s_pref0[(CMP || L2W) ? 2 : 3 * (NM + 1)];
     __shared__ double s_vref0[(CMP || L2W) ? 2 : NM + 1];
     __shared__ double s_x0[6], s_up[2];
@@ -725,8 +732,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                         const int i = 16 * ib + ((t >> 4) & 3) + 4 * reg, j = 16 * jb + mc;
                         if constexpr (FULLP) {
                             if (i <= j && j < NN) {
-                                s_P[i * NN + j] = acc[ti][reg];
-                                s_P[j * NN + i] = acc[ti][reg];
+                                s_P[i * PS + j] = acc[ti][reg];
+                                s_P[j * PS + i] = acc[ti][reg];
                             }
                         } else {
                             if (i <= j && j < NN) s_P[i * NN - (i * (i - 1)) / 2 + (j - i)] = acc[ti][reg];
@@ -751,11 +758,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         // Rds[1] = Rds[2]), so adding each entry once gives the rows the per-entry loop gave.
         if (own) {
             // (FULLP: each upper entry's mirror gets the same sum -- the two were equal bit for bit)
-            const int rb0 = FULLP ? t * NN : t * NN - (t * (t - 1)) / 2 - t;   // row t: P(t, j) at rb0 + j (j >= t)
+            const int rb0 = FULLP ? t * PS : t * NN - (t * (t - 1)) / 2 - t;   // row t: P(t, j) at rb0 + j (j >= t)
             auto addp = [&](int j, double v) {
                 const double nv = s_P[rb0 + j] + v;
                 s_P[rb0 + j] = nv;
-                if constexpr (FULLP) s_P[j * NN + t] = nv;
+                if constexpr (FULLP) s_P[j * PS + t] = nv;
             };
             s_P[rb0 + t] = s_P[rb0 + t] + (2.0 * (ch ? Rs1 : Rs0) + 2.0 * (ch ? Rd1 : Rd0) * dmul);
             if (ch == 0) {
@@ -771,7 +778,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         const int tt = opaque_t();
         if constexpr (FULLP) {
             const int tr = tt < NN ? tt : NN - 1;
-            lds_load_all<NN>(s_P + tr * NN, Prow);
+            lds_load_all<NN>(s_P + tr * PS, Prow);
 #pragma unroll
             for (int j = 0; j < NN; ++j) Prow[j] = own ? Prow[j] : 0.0;
         } else {
@@ -934,7 +941,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         if constexpr (FULLP) {
             // the whole row (symmetric bit for bit: lane t's D_t D_j products equal lane j's), 16-byte stores
             if (t < NN) {
-                double2* const w2 = reinterpret_cast<double2*>(__builtin_assume_aligned(s_P + t * NN, 16));
+                double2* const w2 = reinterpret_cast<double2*>(__builtin_assume_aligned(s_P + t * PS, 16));
 #pragma unroll
                 for (int j = 0; j < NN; j += 2)
                     w2[j / 2] = double2{own ? Prow[j] : ((j == t) ? 1.0 : 0.0),
@@ -967,7 +974,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             if constexpr (FULLP && WAVES > 1) {
                 // contiguous row, ROLLED over blocks of 8 (see below); same products in the same chains
                 const double2* pr2 = reinterpret_cast<const double2*>(
-                    __builtin_assume_aligned(s_P + (tt < NN ? tt : NN - 1) * NN, 16));
+                    __builtin_assume_aligned(s_P + (tt < NN ? tt : NN - 1) * PS, 16));
                 const double2* vb2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb, 16));
 #pragma nounroll
                 for (int c0 = 0; c0 < NN; c0 += 8) {
@@ -993,7 +1000,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             } else if constexpr (FULLP) {
                 // the row and the broadcast in chunks of 8 (16-byte reads), same products in the same chains
                 const double2* pr2 = reinterpret_cast<const double2*>(
-                    __builtin_assume_aligned(s_P + (tt < NN ? tt : NN - 1) * NN, 16));
+                    __builtin_assume_aligned(s_P + (tt < NN ? tt : NN - 1) * PS, 16));
                 const double2* vb2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb, 16));
 #pragma unroll
                 for (int c0 = 0; c0 < NN; c0 += 8) {
@@ -1231,8 +1238,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 // are restored.  Padding rows n..NN-1 hold the identity in s_P; lanes >= NN hold exact zero rows
                 // (the receivers of the one-wave sweep below).
                 const int tt = opaque_t();
-                const int pdg = FULLP ? tt * NN + tt : paddr(tt, tt), psp = FULLP ? tt * NN + tt + 2 : paddr(tt + 2, tt);
-                const int psm = (tt + 2) * NN + tt;   // FULLP: the mirror of (t, t + 2)
+                const int pdg = FULLP ? tt * PS + tt : paddr(tt, tt), psp = FULLP ? tt * PS + tt + 2 : paddr(tt + 2, tt);
+                const int psm = (tt + 2) * PS + tt;   // FULLP: the mirror of (t, t + 2)
                 const bool has_sp = own && (t + 2 < n);
                 double o_dg = 0.0, o_sp = 0.0;
                 if (own) {
@@ -1250,10 +1257,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     const int r = tt - SP2;
                     const int rr = r >= 0 ? r : 0;
 #pragma unroll
-                    for (int j = 0; j < NN; ++j) Krow[j] = (r >= 0) ? s_P[FULLP ? rr * NN + j : paddr(j, rr)] : 0.0;
+                    for (int j = 0; j < NN; ++j) Krow[j] = (r >= 0) ? s_P[FULLP ? rr * PS + j : paddr(j, rr)] : 0.0;
                 } else if constexpr (FULLP) {
                     // (lanes >= NN: exact zero rows, the one-wave sweep's receivers)
-                    lds_load_all<NN>(s_P + (tt < NN ? tt : NN - 1) * NN, Krow);
+                    lds_load_all<NN>(s_P + (tt < NN ? tt : NN - 1) * PS, Krow);
                     if (t >= NN) {
 #pragma unroll
                         for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
