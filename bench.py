@@ -573,10 +573,12 @@ def parse_args(argv=None):
                     help="skip the one-trajectory measurement (configs[0]: drop-in per call, fused B=1, oracle 1 thread)")
     ap.add_argument("--per-step", action="store_true",
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r03.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r04.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
-    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r03.json"),
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r04.json"),
                     help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
+    ap.add_argument("--stall-json", default=os.path.join(HERE, "profiles", "r04_pmc_stall.json"),
+                    help="SQ wave-cycle counters of the fused launch (tools/pmc_stall.sh / pmc_stall.py)")
     ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r03.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
     ap.add_argument("--knet-weights", default=None,
@@ -756,6 +758,18 @@ def bench_run(args, ops, dist, rank, world):
                                                     / (SIMDS * CLOCK_HZ))
         except (OSError, ValueError, KeyError):
             issue = None
+    if issue is not None and os.path.exists(args.stall_json):
+        try:
+            with open(args.stall_json) as f:
+                sc = json.load(f)["counters"]
+            # measured SIMD VALU occupancy of the profiled 20-step launch: SQ_ACTIVE_INST_VALU (quad-cycles, summed
+            # over waves) x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) -- no clock assumption (MI355X_MICROARCH.md)
+            issue["simd_valu_active_frac_pmc"] = sc["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * sc["GRBM_GUI_ACTIVE"] / 8.0)
+            issue["wave_cycle_split_pmc"] = {k: sc[k] / sc["SQ_WAVE_CYCLES"] for k in
+                                             ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")}
+            issue["stall_source"] = os.path.relpath(args.stall_json, HERE)
+        except (OSError, ValueError, KeyError, ZeroDivisionError):
+            pass
     out = {
         "metric": "MPC steps/sec (batch=4096, N=20)" if (B == 4096 and N == 20) else f"MPC steps/sec (batch={B}, N={N})",
         "value": value,

@@ -1,0 +1,56 @@
+/* cdiv (trajectory_generation_amd/csrc/mpc_common.h) against IEEE division on the build host: d / c as
+ * q = d y, t = q c - d (fma), q - t y (fma), y = 1 / c rounded.  Random operands over the whole normal range plus
+ * signed zeros and subnormals; prints mismatches per divisor (exit 1 if any has |d| >= 1e-290).
+ *   gcc -O2 -o /tmp/check_cdiv tools/check_cdiv.c -lm && /tmp/check_cdiv */
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+static uint64_t s = 88172645463325252ULL;
+static uint64_t rnd(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+static double cdiv(double d, double c, double y) {
+    volatile double q = d * y;
+    volatile double t = fma(q, c, -d);
+    volatile double nt = -t;
+    return fma(nt, y, q);
+}
+int main(void) {
+    /* 2 eps (the central differences), OSQP's delta (polish), and every n = 2N the kernels take (the Ruiz mean) */
+    double cs[2 + 256];
+    int nc = 0;
+    cs[nc++] = 2.0 * 1e-5;
+    cs[nc++] = 1e-6;
+    for (int n = 2; n <= 512; n += 2) cs[nc++] = n;
+    const double sp[] = {0.0, -0.0, 1e-320, -1e-320, 4.9e-324, 2.2250738585072014e-308, 1.0, -1.0};
+    long total_bad_normal = 0;
+    for (int ci = 0; ci < nc; ++ci) {
+        const double c = cs[ci], y = 1.0 / c;
+        long bad = 0, bad_sub = 0, n = 0;
+        double dmax = 0.0;
+        for (int k = 0; k < 8; ++k) {
+            const double d = sp[k], q = cdiv(d, c, y), ref = d / c;
+            if (memcmp(&q, &ref, 8)) { if (fpclassify(ref) == FP_SUBNORMAL) ++bad_sub; else ++bad; }
+        }
+        const long ops = ci < 2 ? 60000000 : 4000000;
+        for (long i = 0; i < ops; ++i) {
+            uint64_t bits = rnd();
+            bits &= ~(0x7ffULL << 52);
+            bits |= ((uint64_t)((int)(rnd() % 2046) + 1)) << 52;
+            double d;
+            memcpy(&d, &bits, 8);
+            if (fabs(d) > 1e300) continue;
+            const double q = cdiv(d, c, y), ref = d / c;
+            ++n;
+            if (memcmp(&q, &ref, 8)) {
+                if (fpclassify(ref) == FP_SUBNORMAL) ++bad_sub; else ++bad;
+                if (fabs(d) > dmax) dmax = fabs(d);
+            }
+        }
+        if (ci < 2 || bad || bad_sub || ci % 32 == 0) printf("c = %.17g: %ld operands, %ld mismatches with a normal or zero quotient, %ld subnormal; largest |d| with a "
+               "mismatch %.3g\n", c, n, bad, bad_sub, dmax);
+        if (dmax < 1e-290) bad = 0;   /* remainder underflow only: |d| below 1e-290 */
+        total_bad_normal += bad;
+    }
+    return total_bad_normal ? 1 : 0;
+}

@@ -185,6 +185,33 @@ __device__ __forceinline__ double vmax_abs2(double a, double b) {   // max(|a|, 
     return r;
 }
 
+// A value the compiler cannot see through (an empty asm that "modifies" it): keeps a per-lane mask from being
+// folded back into a branch condition
+__device__ __forceinline__ unsigned opaque_u(unsigned v) {
+    asm volatile("" : "+v"(v));
+    return v;
+}
+// m ? a : b per bit (m all ones or all zeros per lane) as two v_bfi_b32: both operands are formed on every lane
+__device__ __forceinline__ double bitsel(unsigned m, double a, double b) {
+    const unsigned long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+    const unsigned lo = (unsigned(ua) & m) | (unsigned(ub) & ~m);
+    const unsigned hi = (unsigned(ua >> 32) & m) | (unsigned(ub >> 32) & ~m);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// d / c for a constant c with y = 1 / c (rounded) given: q = d y corrected once by the exact remainder
+// (Markstein): r = -(q c - d) by fma, q + r y -- the IEEE quotient bit for bit for d = +-0 and every |d| >= 1e-290
+// (tools/check_cdiv.c: random operands over the whole exponent range for c = 2e-5, 1e-6 and every even 2..512; below
+// that the remainder underflows and the last bit can differ), in 3 f64 operations instead of ~10.  Used for the
+// central differences' (fp - fm) / (2 eps) on every path (the fused and per-step linearizations agree), the
+// polish's quotients by delta and the Ruiz mean's by n.
+__device__ __forceinline__ double cdiv(double d, double c, double y) {
+    double q = d * y, t, r;
+    asm("v_fma_f64 %0, %1, %2, -%3" : "=v"(t) : "v"(q), "v"(c), "v"(d));   // q c - d (exact)
+    asm("v_fma_f64 %0, -%1, %2, %3" : "=v"(r) : "v"(t), "v"(y), "v"(q));   // q - t y
+    return r;
+}
+
 // Three-address fma (v_fma_f64 dst, a, b, c): keeps the compiler from turning a register-rotating
 // update into an in-place v_fmac plus register copies.
 __device__ __forceinline__ double fma3(double a, double b, double c) {

@@ -22,6 +22,8 @@
 
 namespace tgmpc {
 
+constexpr double DQ_INV = 1.0 / (2.0 * 1e-5);   // 1 / (2 eps), rounded: the central differences' cdiv
+
 // f of the nominal rollout (mpc_6stati.py:55-71 with the tire model of :25-53), in the form the fused
 // kernel evaluates lane-parallel (block_linearize): the Pacejka sine taken from sincos, like sin/cos(phi).
 __device__ __forceinline__ void rollout_f(const VP& p, const double* x, double d, double delta, double sd, double cd,
@@ -134,7 +136,7 @@ __device__ __forceinline__ void state_column(const VP& p, const double* xb, doub
            de, sd, cd, fp);
     f_full(p, grp == 0 ? xb[3] - eps : vx, grp == 1 ? xb[4] - eps : vy, grp == 2 ? xb[5] - eps : om, sphi, cphi, d,
            de, sd, cd, fm);
-    for (int r = 0; r < 6; ++r) J[r] = (fp[r] - fm[r]) / (2.0 * eps);
+    for (int r = 0; r < 6; ++r) J[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
 }
 
 // The phi, d and delta columns (Jphi, Jd, Jde), which reuse the base tire evaluation.
@@ -154,12 +156,12 @@ __device__ __forceinline__ void cheap_columns(const VP& p, const double* xb, dou
         pm_sincos(xb[2] - eps, &sm, &cm);
         f_parts(p, vx, vy, om, sp, cp, sd, cd, Ff0, Fr0, Fx0, fp);
         f_parts(p, vx, vy, om, sm, cm, sd, cd, Ff0, Fr0, Fx0, fm);
-        for (int r = 0; r < 6; ++r) Jphi[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        for (int r = 0; r < 6; ++r) Jphi[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
     }
     {   // d: only the longitudinal force changes
         f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d + eps), fp);
         f_parts(p, vx, vy, om, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx, d - eps), fm);
-        for (int r = 0; r < 6; ++r) Jd[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        for (int r = 0; r < 6; ++r) Jd[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
     }
     {   // delta: front force and sin/cos(delta) change
         double sp, cp, sm, cm;
@@ -167,7 +169,7 @@ __device__ __forceinline__ void cheap_columns(const VP& p, const double* xb, dou
         pm_sincos(de - eps, &sm, &cm);
         f_parts(p, vx, vy, om, sphi, cphi, sp, cp, front_force(p, t0.atf, de + eps), Fr0, Fx0, fp);
         f_parts(p, vx, vy, om, sphi, cphi, sm, cm, front_force(p, t0.atf, de - eps), Fr0, Fx0, fm);
-        for (int r = 0; r < 6; ++r) Jde[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        for (int r = 0; r < 6; ++r) Jde[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
     }
     // a -0.0 among the components the input columns pass through: evaluate those two columns on
     // the reference's exact vectors, f(x, u +- du) with u_other + 0.0 (signed zeros match too)
@@ -181,7 +183,7 @@ __device__ __forceinline__ void cheap_columns(const VP& p, const double* xb, dou
             for (int i = 0; i < 6; ++i) xc[i] = xb[i];
             f_cont(p, xc, up, fp);
             f_cont(p, xc, um, fm);
-            for (int r = 0; r < 6; ++r) (cu == 0 ? Jd : Jde)[r] = (fp[r] - fm[r]) / (2.0 * eps);
+            for (int r = 0; r < 6; ++r) (cu == 0 ? Jd : Jde)[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
         }
     }
 }
@@ -289,18 +291,27 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
         const double dlt = (t == 17) ? u1 + eps : ((t == 18) ? u1 - eps : u1);
         const double pz = (t == 19) ? eps : ((t == 20) ? -eps : 0.0);
         const double Bt = fr ? p.Bf : p.Br, Ct = fr ? p.Cf : p.Cr;
+        // The roles as per-lane constants, so the stage body is one branch-free instruction stream: the
+        // evaluation point is x_i + d_i with d_i = -0.0 on the rollout lanes (x + -0.0 = x for every x, -0.0
+        // included), 0.0 for the base evaluations (x_i + 0.0) and +-eps for a column's perturbed component; the
+        // rear tire's "oml lr - vyl" as oml lr + (-1 vyl) and its alpha "at" as 1 at + -0.0 (exact identities)
+        const double dvx = roll ? -0.0 : (col == 0 ? sgn : 0.0);
+        const double dvy = roll ? -0.0 : (col == 1 ? sgn : 0.0);
+        const double dom = roll ? -0.0 : (col == 2 ? sgn : 0.0);
+        const double Lt = fr ? p.lf : p.lr, sy = fr ? 1.0 : -1.0, sa = fr ? -1.0 : 1.0, dl = fr ? dlt : -0.0;
+        const double dz = (t == 2) ? -0.0 : pz;
+        const unsigned mtire = opaque_u(tire ? 0xffffffffu : 0u);
         for (int k = 0; k < N; ++k) {
             const double phi = x[2], vx = x[3], vy = x[4], omega = x[5];
             // this lane's evaluation point (state_column / cheap_columns: x_i + 0.0, the column x_i +- eps)
-            const double vxl = roll ? vx : (col == 0 ? vx + sgn : vx + 0.0);
-            const double vyl = roll ? vy : (col == 1 ? vy + sgn : vy + 0.0);
-            const double oml = roll ? omega : (col == 2 ? omega + sgn : omega + 0.0);
+            const double vxl = vx + dvx, vyl = vy + dvy, oml = omega + dom;
             const double avx = fabs(vxl);
             const double mx = (p.vx_zero > avx) ? p.vx_zero : avx;
             const double vx_eff = np_sign(vxl) * mx;
-            const double at = pm_atan2(fr ? oml * p.lf + vyl : oml * p.lr - vyl, vx_eff);
-            const double alpha = clampd(fr ? -at + dlt : at, -p.maxAlpha, p.maxAlpha);
-            const double z = tire ? Ct * pm_atan(Bt * alpha) : (t == 2 ? phi : phi + pz);
+            const double at = pm_atan2(oml * Lt + sy * vyl, vx_eff);
+            const double alpha = clampd(sa * at + dl, -p.maxAlpha, p.maxAlpha);
+            // tire lanes: Ct atan(Bt alpha); the sincos lanes: phi + dz (a bitwise select: no branch)
+            const double z = bitsel(mtire, Ct * pm_atan(Bt * alpha), phi + dz);
             double sz, cz;
             pm_sincos(z, &sz, &cz);
             if (t >= 3 && t <= 21) tj[LREC * k + t] = sz;
@@ -348,21 +359,21 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
             const int l = 5 + 4 * grp;
             f_parts(p, vxp, vyp, omp, sphi, cphi, sd, cd, p.Df * T[l], p.Dr * T[l + 1], long_force(p, vxp, d), fp);
             f_parts(p, vxm, vym, omm, sphi, cphi, sd, cd, p.Df * T[l + 2], p.Dr * T[l + 3], long_force(p, vxm, d), fm);
-            for (int r = 0; r < 6; ++r) Ak[6 * r + 3 + grp] = a_entry(r, 3 + grp, Ts, (fp[r] - fm[r]) / (2.0 * eps));
+            for (int r = 0; r < 6; ++r) Ak[6 * r + 3 + grp] = a_entry(r, 3 + grp, Ts, cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV));
         }
         double Jphi[6], Jd[6], Jde[6];
         // phi: only sin / cos(phi) change
         f_parts(p, vx0, vy0, om0, T[19], T[0], sd, cd, Ff0, Fr0, Fx0, fp);
         f_parts(p, vx0, vy0, om0, T[20], T[1], sd, cd, Ff0, Fr0, Fx0, fm);
-        for (int r = 0; r < 6; ++r) Jphi[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        for (int r = 0; r < 6; ++r) Jphi[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
         // d: only the longitudinal force changes
         f_parts(p, vx0, vy0, om0, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx0, d + eps), fp);
         f_parts(p, vx0, vy0, om0, sphi, cphi, sd, cd, Ff0, Fr0, long_force(p, vx0, d - eps), fm);
-        for (int r = 0; r < 6; ++r) Jd[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        for (int r = 0; r < 6; ++r) Jd[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
         // delta: front force and sin / cos(delta) change
         f_parts(p, vx0, vy0, om0, sphi, cphi, sdp, cdp, p.Df * T[17], Fr0, Fx0, fp);
         f_parts(p, vx0, vy0, om0, sphi, cphi, sdm, cdm, p.Df * T[18], Fr0, Fx0, fm);
-        for (int r = 0; r < 6; ++r) Jde[r] = (fp[r] - fm[r]) / (2.0 * eps);
+        for (int r = 0; r < 6; ++r) Jde[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
         // a -0.0 among the components the input columns pass through: those two columns on the
         // reference's exact vectors, as cheap_columns does
         if ((__builtin_signbit(xb[2]) && xb[2] == 0.0) || (__builtin_signbit(xb[3]) && xb[3] == 0.0) ||
@@ -375,7 +386,7 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
                 for (int i = 0; i < 6; ++i) xc[i] = xb[i];
                 f_cont(p, xc, up, fp);
                 f_cont(p, xc, um, fm);
-                for (int r = 0; r < 6; ++r) (cu == 0 ? Jd : Jde)[r] = (fp[r] - fm[r]) / (2.0 * eps);
+                for (int r = 0; r < 6; ++r) (cu == 0 ? Jd : Jde)[r] = cdiv(fp[r] - fm[r], 2.0 * eps, DQ_INV);
             }
         }
         for (int r = 0; r < 6; ++r) {

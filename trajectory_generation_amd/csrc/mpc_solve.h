@@ -347,8 +347,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // ---- block helpers -------------------------------------------------------------
     auto exch = [&](double v, int delta) -> double {   // value of variable t+delta (0 outside)
         if constexpr (WAVES == 1) {
-            // delta is +-2 at every call site: two DPP wave shifts, no LDS round trip
-            const double vm = own ? v : 0.0;
+            // delta is +-2 at every call site: two DPP wave shifts, no LDS round trip.  Shifting down, an own
+            // lane t >= 2 reads own lane t - 2 and lanes 0, 1 get the DPP bound's 0, so only the upward shift
+            // zeroes the source (lanes n, n + 1 feed own lanes n - 2, n - 1)
+            const double vm = (delta > 0 && !own) ? 0.0 : v;
             const double r = (delta > 0) ? lane_up2(vm) : lane_dn2(vm);
             return own ? r : 0.0;
         } else {
@@ -849,6 +851,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             for (int j = 0; j < NN; ++j) c4[j & 3] = vmax_abs(c4[j & 3], Prow[j]);
             cn = vmax(vmax(c4[0], c4[1]), vmax(c4[2], c4[3]));
         }
+        const double ninv = 1.0 / n;   // (the mean column norm: cdiv, mpc_common.h)
         for (int it = 0; it < c.scaling_iters; ++it) {
             double Er_up = exch(Er, +2);     // E of rate row t+2
             double D_dn = exch(D, -2);       // D of variable t-2
@@ -881,7 +884,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             Eb *= Etb;
             Er *= Etr;
             // cost scaling of the scaled data cs (P, q)
-            double mean = block_sum(own ? cs * cn : 0.0) / n;
+            double mean = cdiv(block_sum(own ? cs * cn : 0.0), (double)n, ninv);
             double qv[1] = {own ? fabs(cs * qi) : 0.0};
             block_max(qv);
             double ct = fmax(mean, limit_scaling(qv[0]));
@@ -1186,6 +1189,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         int rounds = 0, ps = 0, actb = 0, actr = 0;
         double escale = 1.0;
         const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
+        const double dlinv = 1.0 / dl;   // (quotients by delta: cdiv, mpc_common.h)
         iter = 1;
         int nfact = 0;
         // diagnostics (traj_debug_set_stamps): cycles in residual checks / sweeps / polish
@@ -1223,8 +1227,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             stash();
             reload();
             // ---- build K (row t) ----
-            const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
-            const double kr = (phase == PH_ADMM) ? rr : (actr ? 1.0 / dl : 0.0);
+            const double kb = (phase == PH_ADMM) ? rb : (actb ? dlinv : 0.0);
+            const double kr = (phase == PH_ADMM) ? rr : (actr ? dlinv : 0.0);
             const double ks = (phase == PH_ADMM) ? sig : dl;
             {
                 const double kr_up = exch(kr, +2);
@@ -1651,12 +1655,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 double r1 = -qi, r2b = actb ? bb : 0.0, r2r = actr ? br : 0.0;
                 double axb = 0.0, axr = 0.0;
                 for (int rf = 0; rf <= c.polish_refine_iter; ++rf) {
-                    double tv = Kmul(r1 + ATw(actb ? r2b / dl : 0.0, actr ? r2r / dl : 0.0));
+                    double tv = Kmul(r1 + ATw(actb ? cdiv(r2b, dl, dlinv) : 0.0, actr ? cdiv(r2r, dl, dlinv) : 0.0));
                     double tb, tr;
                     Ax(tv, tb, tr);
                     px_ += tv;
-                    if (actb) pyb += (tb - r2b) / dl;
-                    if (actr) pyr += (tr - r2r) / dl;
+                    if (actb) pyb += cdiv(tb - r2b, dl, dlinv);
+                    if (actr) pyr += cdiv(tr - r2r, dl, dlinv);
                     if (rf == c.polish_refine_iter) break;
                     double Pxv = Pmul(px_);
                     double atyv = ATw(pyb, pyr);
