@@ -5,6 +5,8 @@ set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
 tag=${TAG:-combo}
+timeout -k 10 60 ./tools/microbench/check_ops.bin > gpurun_out/r4_${tag}_check_ops.log 2>&1 || { cat gpurun_out/r4_${tag}_check_ops.log; exit 1; }
+cat gpurun_out/r4_${tag}_check_ops.log
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread \
   > gpurun_out/r4_${tag}_tests.log 2>&1 || { tail -30 gpurun_out/r4_${tag}_tests.log; exit 1; }
 tail -2 gpurun_out/r4_${tag}_tests.log

@@ -199,6 +199,33 @@ __device__ __forceinline__ double bitsel(unsigned m, double a, double b) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// sqrt(x) for finite x >= 2^-767 (and NaN): the instruction sequence the compiler lowers sqrt to on gfx950 -- v_rsq_f64
+// and two Newton / Goldschmidt corrections -- without its range scaling (x < 2^-767) and its +-0 / +inf class
+// fix-up, so the same value in 10 instead of 17 VALU (tools/microbench/check_ops.hip compares the two on the GPU).
+// The Ruiz pass's arguments are limit_scaling()'s, in [1e-4, 1e4].
+__device__ __forceinline__ double sqrt_n(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    const double d0 = fma(-g, g, x);
+    h = fma(h, r, h);
+    g = fma(d0, h, g);
+    const double d1 = fma(-g, g, x);
+    return fma(d1, h, g);
+}
+// 1 / b where the division needs no operand scaling (b normal, |b| well inside [2^-900, 2^900]): the compiler's
+// f64 division sequence without v_div_scale / v_div_fmas scaling / v_div_fixup -- the same value in 8 VALU, not 11
+__device__ __forceinline__ double rcp_n(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    const double r = fma(-b, y, 1.0);
+    return fma(r, y, y);
+}
+
 // d / c for a constant c with y = 1 / c (rounded) given: q = d y corrected once by the exact remainder
 // (Markstein): r = -(q c - d) by fma, q + r y -- the IEEE quotient bit for bit for d = +-0 and every |d| >= 1e-290
 // (tools/check_cdiv.c: random operands over the whole exponent range for c = 2e-5, 1e-6 and every even 2..512; below

@@ -858,9 +858,10 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
             const double pn = cs * cn;
             double coln = vmax(pn, vmax_abs(vmax_abs2(a_b, a_r), a_rp));
-            double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
-            double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
-            double Etr = 1.0 / sqrt(limit_scaling(vmax_abs2(a_r, a_rm)));
+            // (limit_scaling keeps the arguments in [1e-4, 1e4]: sqrt_n / rcp_n are sqrt and 1 / x bit for bit there)
+            double Dt = own ? rcp_n(sqrt_n(limit_scaling(coln))) : 1.0;
+            double Etb = rcp_n(sqrt_n(limit_scaling(fabs(a_b))));
+            double Etr = rcp_n(sqrt_n(limit_scaling(vmax_abs2(a_r, a_rm))));
             // the broadcast D read in chunks of RCH, each chunk's reads in flight at once (CMP: 8, so that the
             // row of P and the chunk fit the 3-wave register budget; otherwise the whole vector)
             const double* dvb = bcast(Dt);
@@ -888,7 +889,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double qv[1] = {own ? fabs(cs * qi) : 0.0};
             block_max(qv);
             double ct = fmax(mean, limit_scaling(qv[0]));
-            ct = 1.0 / limit_scaling(ct);
+            ct = rcp_n(limit_scaling(ct));
             cs *= ct;
         }
 #pragma unroll
