@@ -1,5 +1,7 @@
 // mpc_inst.hip -- one translation unit per horizon capacity (compiled with -DTGMPC_NN=<NN>), so
 // the fully unrolled instantiations of the MPC kernels build in parallel.
+#include <atomic>
+
 #include "mpc_launch.h"
 
 #ifndef TGMPC_NN
@@ -13,6 +15,7 @@ namespace tgmpc {
 
 #if TGMPC_NN == 40
 int launch_fused_w3_40(const KArgs& a, hipStream_t st);   // mpc_inst_w3.hip
+void preload_fused_w3_40();                                // mpc_inst_w3.hip
 #endif
 
 // mode 0: MPC step, 1: QP only (A/B/g given), 2: closed-loop step (the linearization launches are
@@ -23,6 +26,20 @@ int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
     dim3 grid(a.B), sblock(((NN + 63) / 64) * 64);
     if (mode == 3) {
 #if TGMPC_NN == 40
+        {
+            // HIP loads a kernel's code object at its first launch (milliseconds of host time for these): the first
+            // fused launch at this capacity loads BOTH instances, so a later long launch (the 3-wave one, e.g. the
+            // configs[3] dataset leg after a 20-step run) does not pay it inside its own call.  Per device.
+            static std::atomic<bool> loaded[64];
+            int dev = 0;
+            if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && !loaded[dev].load()) {
+                hipFuncAttributes fa;
+                preload_fused_w3_40();
+                if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&solve_kernel<NN, true, true, false, 2>)) ==
+                    hipSuccess)
+                    loaded[dev].store(true);
+            }
+        }
         if (a.wps == 3) return launch_fused_w3_40(a, st);
 #endif
 #if TGMPC_NN > 64

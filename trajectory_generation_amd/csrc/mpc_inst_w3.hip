@@ -9,4 +9,10 @@ namespace tgmpc {
 
 int launch_fused_w3_40(const KArgs& a, hipStream_t st) { return launch_fused<40, 3>(a, st); }
 
+// load the instance's code object without launching it (mpc_inst.hip's first fused launch at capacity 40)
+void preload_fused_w3_40() {
+    hipFuncAttributes fa;
+    (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&solve_kernel<40, true, true, false, 3>));
+}
+
 }  // namespace tgmpc
