@@ -1087,7 +1087,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double v[8];
             if (own) {
                 double dres = px + qi + aty;
-                const double Dinv = 1.0 / cold(C_D), Ebinv = 1.0 / cold(C_EB), Erinv = 1.0 / cold(C_ER);
+                const double Dinv = rcp_n(cold(C_D)), Ebinv = rcp_n(cold(C_EB)), Erinv = rcp_n(cold(C_ER));
                 v[0] = vmax_abs2(Ebinv * (axb - zb), Erinv * (axr - zr));   // prim res
                 v[1] = vmax(vmax_abs2(Ebinv * axb, Erinv * axr), vmax_abs2(Ebinv * zb, Erinv * zr));
                 v[2] = fabs(Dinv * dres) * csinv;
@@ -1585,7 +1585,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     double zrb = fma(alpha, ztb, oma * zb);
                     double zrr = fma(alpha, ztr, oma * zr);
                     const dpair ri = pair(P_RHOI), bb = pair(P_BB), br = pair(P_BR);   // (LDS, see the cold values)
-                    double nzb = clampd(fma(ri.x, yb, zrb), bb.x, bb.y), nzr = clampd(fma(ri.y, yr, zrr), br.x, br.y);
+                    double nzb = clamp_mm(fma(ri.x, yb, zrb), bb.x, bb.y), nzr = clamp_mm(fma(ri.y, yr, zrr), br.x, br.y);
                     yb = fma(rb, zrb - nzb, yb);
                     yr = fma(rr, zrr - nzr, yr);
                     x = xn;
