@@ -60,7 +60,11 @@
 #define TGMPC_PMUL80 1         // capacity 80, one wave per SIMD: the rolled P v of the 3-wave instance
 #endif
 #ifndef TGMPC_SWEEP_UNROLL
-#define TGMPC_SWEEP_UNROLL 4   // one-wave sweep: pivots per unrolled loop body (1: rolled, NN register moves per pivot)
+#define TGMPC_SWEEP_UNROLL 8   // one-wave sweep, fused instances: pivots per unrolled loop body (1: rolled, NN register
+                               // moves per pivot; 8: +0.9 % over 4 at 20 steps, r04)
+#endif
+#ifndef TGMPC_SWEEP_UNROLL_STEP
+#define TGMPC_SWEEP_UNROLL_STEP 4   // the same for the per-step kernels (8 there spills 20-24 B/lane)
 #endif
 #ifndef TGMPC_SWEEP_UNROLL2
 #define TGMPC_SWEEP_UNROLL2 4  // two-wave sweep (capacity 80): the same
@@ -1319,7 +1323,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 }
                 // unrolled by TGMPC_SWEEP_UNROLL: the register rotation is static inside the unrolled body, so
                 // realigning the row costs NN register moves per TGMPC_SWEEP_UNROLL pivots instead of per pivot
-                TGMPC_PRAGMA(unroll TGMPC_SWEEP_UNROLL)
+                constexpr int SWU = FUSED ? TGMPC_SWEEP_UNROLL : TGMPC_SWEEP_UNROLL_STEP;
+#pragma unroll SWU
                 for (int pv = 0; pv < NN; ++pv) {
                     if (NN > SPARE && pv == SPARE) {
                         // lanes 0..SPARE-1 all pivoted (dropped rows): zero them, they receive next
