@@ -92,6 +92,10 @@
 #ifndef TGMPC_RECV2_L2W
 #define TGMPC_RECV2_L2W 1      // L2W: the receiver sweep as well (scratch 1,864 -> 396 B/lane; still opt-in)
 #endif
+#ifndef TGMPC_RUIZ_CUM
+#define TGMPC_RUIZ_CUM 0       // capacity <= 40: Ruiz norms from the cumulative scaling, the row scaled once (measured
+                               // neutral at 20 steps, r04: off, keeping OSQP's in-place order)
+#endif
 #ifndef TGMPC_PSPAD
 #define TGMPC_PSPAD 2          // FULLP: row stride NN + TGMPC_PSPAD doubles (0: NN, the bank-conflicted stride)
 #endif
@@ -165,6 +169,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     constexpr int PS = FULLP ? NN + TGMPC_PSPAD : NN;
     static_assert(!FULLP || TGMPC_PSPAD != 2 || (2 * PS) % 8 == 4, "conflict-free row stride");
     constexpr int NP = FULLP ? NN * PS : NP0;
+    // cumulative Ruiz scaling (the scaling pass) up to capacity 40; the N = 40 problems (condition ~1e9) keep OSQP's
+    // in-place order -- their exact-mode parity bar for unpolished points (0.1) did not hold with it
+    constexpr bool RUIZ_CUM = TGMPC_RUIZ_CUM && NN <= 40;
     __shared__ double s_pref0[(CMP || L2W) ? 2 : 3 * (NM + 1)];
     __shared__ double s_vref0[(CMP || L2W) ? 2 : NM + 1];
     __shared__ double s_x0[6], s_up[2];
@@ -856,6 +863,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             cn = vmax(vmax(c4[0], c4[1]), vmax(c4[2], c4[3]));
         }
         const double ninv = 1.0 / n;   // (the mean column norm: cdiv, mpc_common.h)
+        const double* dvb_last = nullptr;   // RUIZ_CUM: the last pass's broadcast of D
         for (int it = 0; it < c.scaling_iters; ++it) {
             double Er_up = exch(Er, +2);     // E of rate row t+2
             double D_dn = exch(D, -2);       // D of variable t-2
@@ -868,10 +876,29 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             double Etr = rcp_n(sqrt_n(limit_scaling(vmax_abs2(a_r, a_rm))));
             // the broadcast D read in chunks of RCH, each chunk's reads in flight at once (CMP: 8, so that the
             // row of P and the chunk fit the 3-wave register budget; otherwise the whole vector)
-            const double* dvb = bcast(Dt);
             double c4[4] = {0.0, 0.0, 0.0, 0.0};
             constexpr int RCH = (CMP || LEAN || (WAVES > 1 && TGMPC_RCH80)) ? 8 : NN;
             static_assert(NN % RCH == 0, "chunked broadcast");
+            if constexpr (RUIZ_CUM) {
+            // The row stays the unscaled P row; the pass's norms come from the CUMULATIVE scaling:
+            // max_j |P_tj D_j| D_t (one product and one max per entry instead of two products and a max); the row
+            // is scaled once after the last pass, P_tj (D_t D_j) cs -- symmetric bit for bit, as the full-P image
+            // and the packed triangle need.  (OSQP scales P in place every pass; the scaled P agrees to the last
+            // bits, the parity tests' bar.)
+            D *= Dt;
+            const double* dvb = bcast(D);
+            dvb_last = dvb;
+#pragma unroll
+            for (int c0 = 0; c0 < NN; c0 += RCH) {
+                double Dv[RCH];
+                lds_load_all<RCH>(dvb + c0, Dv);
+#pragma unroll
+                for (int j = 0; j < RCH; ++j) c4[(c0 + j) & 3] = vmax_abs(c4[(c0 + j) & 3], Prow[c0 + j] * Dv[j]);
+            }
+            cn = D * vmax(vmax(c4[0], c4[1]), vmax(c4[2], c4[3]));
+            qi *= Dt;
+            } else {
+            const double* dvb = bcast(Dt);
 #pragma unroll
             for (int c0 = 0; c0 < NN; c0 += RCH) {
                 double Dv[RCH];
@@ -886,6 +913,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             cn = vmax(vmax(c4[0], c4[1]), vmax(c4[2], c4[3]));
             qi *= Dt;
             D *= Dt;
+            }
             Eb *= Etb;
             Er *= Etr;
             // cost scaling of the scaled data cs (P, q)
@@ -896,8 +924,24 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             ct = rcp_n(limit_scaling(ct));
             cs *= ct;
         }
+        if constexpr (RUIZ_CUM) {
+            if (dvb_last) {   // the last pass's broadcast of the final D (no LDS write since)
+                constexpr int RCH = (CMP || LEAN) ? 8 : NN;
 #pragma unroll
-        for (int j = 0; j < NN; ++j) Prow[j] *= cs;
+                for (int c0 = 0; c0 < NN; c0 += RCH) {
+                    double Dv[RCH];
+                    lds_load_all<RCH>(dvb_last + c0, Dv);
+#pragma unroll
+                    for (int j = 0; j < RCH; ++j) Prow[c0 + j] = (Prow[c0 + j] * (D * Dv[j])) * cs;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < NN; ++j) Prow[j] *= cs;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < NN; ++j) Prow[j] *= cs;
+        }
         qi *= cs;
         const double csinv = uniformize(1.0 / cs);   // uniform (held in SGPRs, not in VGPRs)
         const double D_dn = exch(D, -2);
