@@ -763,7 +763,7 @@ def bench_run(args, ops, dist, rank, world):
                                                     / (SIMDS * CLOCK_HZ))
         except (OSError, ValueError, KeyError):
             issue = None
-    if issue is not None and os.path.exists(args.stall_json):
+    if issue is not None and fused and N == 20 and B == 4096 and os.path.exists(args.stall_json):   # (the profiled config)
         try:
             with open(args.stall_json) as f:
                 sc = json.load(f)["counters"]
