@@ -533,7 +533,7 @@ def dataset_leg(args, w, ops, dist, rank, world):
             Xa, Ua, sta = D.unpack_history(full)
             t3 = time.perf_counter()
             D._write_with_sidecar(os.path.join(args.dataset_csv, "vehicle_mpc"), Xa, Ua, sta, np.arange(Xa.shape[0]),
-                                  Ts, True)
+                                  Ts, False)
             csv_s = time.perf_counter() - t3
         bar()
         t4 = time.perf_counter()
@@ -550,9 +550,9 @@ def dataset_leg(args, w, ops, dist, rank, world):
             "trajectories": world * B, "steps": T, "traj_steps_per_s": n / gen_s, "generate_s": gen_s,
             "gather_s": gather_s, "gather_bytes": int(full.numel() * full.element_size()),
             "csv_s": csv_s, "csv_shards_s": shard_s,
-            "csv_note": (f"{n_failed} of {world * B} trajectories have a failed step (status >= 2); the gathered CSV "
-                         "(dataset.generate's default, merge_datasets.py:41-47's filter) leaves them out and "
-                         "re-indexes the rest, its status sidecar keeps the generation ids"
+            "csv_note": (f"{n_failed} of {world * B} trajectories have a failed step (status >= 2, u_prev kept as "
+                         "mpc_6stati.py:257-262 does); the CSVs hold every trajectory as the reference generators write "
+                         "them (dataset.generate's default), the status sidecar flags the failed ones"
                          + ("; csv_s: rank 0 writes the gathered CSVs + status sidecar; csv_shards_s: every rank "
                             "writes its own shard (no gather, failed ones flagged in the sidecar), max over ranks"
                             if args.dataset_csv else "")),

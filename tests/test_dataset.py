@@ -78,7 +78,7 @@ def _worker(rank, world, port, q, out_prefix, shards=False):
 
 def test_generate_two_ranks_gloo(tmp_path):
     """dataset.generate at world size 2 (gloo): rank r runs ids [r B, (r+1) B) (the workload's own id
-    offset, merge_datasets.py:41-47 semantics), the packed histories and statuses reach rank 0 only,
+    offset; merge_datasets.py:41-47 offsets ids the same way), the packed histories and statuses reach rank 0 only,
     in id order, and rank 0 writes the CSVs with the global trajectory ids."""
     from trajectory_generation_amd.workload import make_workload
     ctx = mp.get_context("spawn")
@@ -165,7 +165,12 @@ def test_status_sidecar_and_failed_trajectory_filter(tmp_path):
     assert sc["first_failed_step"].tolist() == [-1, -1, 1, -1, 3, -1]
     assert list(pd.read_csv(p1 + "_clean.csv").columns) == D.CLEAN_COLUMNS   # schema unchanged
     p2 = str(tmp_path / "ok")
-    D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p2, closed_loop=_status_closed_loop)   # default: dropped
+    p0 = str(tmp_path / "dflt")
+    D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p0, closed_loop=_status_closed_loop)   # default: all written
+    assert pd.read_csv(p0 + "_status.csv")["trajectory_id"].tolist() == list(range(B))
+    assert (tmp_path / "dflt_clean.csv").read_bytes() == (tmp_path / "all_clean.csv").read_bytes()
+    with pytest.warns(UserWarning, match="left out 2 of 6"):
+        D.generate(B, T, N=20, Ts=0.05, seed=3, out_prefix=p2, closed_loop=_status_closed_loop, drop_failed=True)
     sc2 = pd.read_csv(p2 + "_status.csv")
     assert sc2["trajectory_id"].tolist() == [0, 1, 2, 3] and sc2["source_id"].tolist() == [0, 1, 3, 5]
     assert (sc2["n_failed_steps"] == 0).all()

@@ -85,8 +85,9 @@ def gather_to_root(blk, dist=None, dst=0):
     """The dataset's one collective: every rank's fixed-size [B,T+1,9] block goes to
     rank `dst` only (dist.gather -- RCCL over xGMI with the nccl backend, gloo on CPU).  Returns the
     concatenation in rank order (= global trajectory-id order, ids are rank * B + i) on `dst`, None on
-    the other ranks; the block itself without a process group."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    the other ranks; the block itself without a process group.  With a process group the gather runs at
+    every world size, 1 included (the same collective path as on 8 GPUs)."""
+    if dist is None or not dist.is_initialized():
         return blk
     import torch
     blk = blk.contiguous()
@@ -135,17 +136,17 @@ def _closed_loop_gpu(w, T, cfg):
 
 
 def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=None, polish_mode=0,
-             closed_loop=None, drop_failed=None, shards=False):
+             closed_loop=None, drop_failed=False, shards=False):
     """Run the closed loop for this rank's B trajectories (ids rank * B .. rank * B + B - 1), gather the
     histories to rank 0 and (rank 0) write ``{out_prefix}_clean.csv`` / ``{out_prefix}_noisy.csv`` and the
     status sidecar ``{out_prefix}_status.csv`` (write_status_csv).
 
-    drop_failed: leave out every trajectory with a failed step (status >= 2) and re-index the rest 0..n-1 (the
-      ids data_loader.py expects, merge_datasets.py:41-47's filter and re-indexing) -- each keeps the noise of its
-      generation id, which the sidecar's source_id column records.  Default (None): on with the gather, so a
-      diverged trajectory never lands silently in a training CSV; with shards=True (no gather to re-index
-      across ranks) every trajectory is written and the sidecar flags the failed ones.  False writes all of
-      them with the gather too (the reference generators' own behaviour).
+    drop_failed: opt-in (default False, the reference generators' behaviour: generation_type1.py:295-339 writes
+      every trajectory, a failed step having kept u_prev as mpc_6stati.py:257-262 returns it; merge_datasets.py
+      only offsets the ids of its second file, :41-47, and filters nothing).  True leaves out every trajectory
+      with a failed step (status >= 2) and re-indexes the rest 0..n-1 (the contiguous ids data_loader.py reads) --
+      each keeps the noise of its generation id, which the sidecar's source_id column records; a warning names
+      how many were dropped.  Either way the status sidecar flags the failed trajectories.
     shards: no gather -- every rank writes its own ``{out_prefix}_rank{r}_*.csv`` (global ids; the shards'
       bodies concatenated in rank order are the single file's body) and its sidecar (SURVEY.md 8(e)'s
       per-rank alternative); returns this rank's share on every rank.
@@ -161,8 +162,6 @@ def generate(B, T, N=20, Ts=0.05, kind="spline", seed=0, out_prefix=None, dist=N
         from . import batch as TB
         cfg = TB.config_struct(N=N, Ts=Ts, polish_mode=polish_mode)
         closed_loop = _closed_loop_gpu
-    if drop_failed is None:
-        drop_failed = not shards
     if shards and drop_failed:
         raise ValueError("drop_failed re-indexes the whole dataset: it needs the gather (shards=False)")
     res = closed_loop(w, T, cfg)
@@ -188,6 +187,10 @@ def _write_with_sidecar(prefix, X, U, st, ids, Ts, drop_failed):
     ids = np.asarray(ids, dtype=np.int64)
     if drop_failed:
         keep = np.nonzero((sth >= FAILED_STATUS).sum(axis=0) == 0)[0]
+        if keep.size < ids.size:
+            import warnings
+            warnings.warn(f"{prefix}: drop_failed left out {ids.size - keep.size} of {ids.size} trajectories with a "
+                          "failed step and re-indexed the rest (their generation ids: the _status.csv source_id)")
         out_ids = np.arange(keep.size, dtype=np.int64)
         write_csv(prefix, Xh[keep], Uh[keep], out_ids, Ts, noise_ids=ids[keep])
         write_status_csv(prefix, sth[:, keep], out_ids, source_ids=ids[keep])
