@@ -30,6 +30,9 @@ pytestmark = pytest.mark.gpu
 TB = pytest.importorskip("trajectory_generation_amd.batch")
 
 
+MAX_ITER = 10000   # traj_mpc_config / OSQP max_iter (CVXPY's default)
+
+
 def rel(a, b):
     return np.max(np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b))))
 
@@ -99,7 +102,10 @@ def _agreement(g, r, both_pol_tol, neither_tol, flag_agree, iters_equal):
     du = np.abs(g["U_opt"] - r["U_opt"]).max(axis=(1, 2))
     both = pg & pr & ok
     assert du[both].max(initial=0.0) <= both_pol_tol
-    neither = ~pg & ~pr & (g["status"] == 0)
+    # (an instance that ran to the 10,000-iteration cap -- exact mode's continuation round keeps "optimal" there when
+    # the base eps is met -- stopped at no converged point: a 2-ulp change of the tire sine alone moves the oracle's own
+    # cap point by 0.12 at N = 40, so it is compared by status and iteration count only)
+    neither = ~pg & ~pr & (g["status"] == 0) & (g["iters"] < MAX_ITER)
     assert du[neither].max(initial=0.0) <= neither_tol
     dobj = np.abs(g["objective"] - r["objective"]) / np.abs(r["objective"])
     assert dobj[both].max(initial=0.0) <= 1e-7

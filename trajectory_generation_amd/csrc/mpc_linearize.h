@@ -24,8 +24,8 @@ namespace tgmpc {
 
 constexpr double DQ_INV = 1.0 / (2.0 * 1e-5);   // 1 / (2 eps), rounded: the central differences' cdiv
 
-// f of the nominal rollout (mpc_6stati.py:55-71 with the tire model of :25-53), in the form the fused
-// kernel evaluates lane-parallel (block_linearize): the Pacejka sine taken from sincos, like sin/cos(phi).
+// f of the nominal rollout (mpc_6stati.py:55-71 with the tire model of :25-53); the Pacejka sine is pm_tire_sin,
+// as on every path.
 __device__ __forceinline__ void rollout_f(const VP& p, const double* x, double d, double delta, double sd, double cd,
                                           double* xd) {
     const double phi = x[2], vx = x[3], vy = x[4], omega = x[5];
@@ -34,9 +34,9 @@ __device__ __forceinline__ void rollout_f(const VP& p, const double* x, double d
     const double vx_eff = np_sign(vx) * mx;
     const double alpha_f = clampd(-pm_atan2(omega * p.lf + vy, vx_eff) + delta, -p.maxAlpha, p.maxAlpha);
     const double alpha_r = clampd(pm_atan2(omega * p.lr - vy, vx_eff), -p.maxAlpha, p.maxAlpha);
-    double sf, cf, sr, cr, sphi, cphi;
-    pm_sincos(p.Cf * pm_atan(p.Bf * alpha_f), &sf, &cf);
-    pm_sincos(p.Cr * pm_atan(p.Br * alpha_r), &sr, &cr);
+    double sphi, cphi;
+    const double sf = pm_tire_sin(p.Cf * pm_atan(p.Bf * alpha_f));
+    const double sr = pm_tire_sin(p.Cr * pm_atan(p.Br * alpha_r));
     pm_sincos(phi, &sphi, &cphi);
     const double Fy_f = p.Df * sf, Fy_r = p.Dr * sr;
     const double Frx = (p.Cm1 - p.Cm2 * vx) * d - p.Cr0 - p.Cr2 * (vx * vx);
@@ -86,13 +86,8 @@ __device__ __forceinline__ Tire tire_angles(const VP& p, double vx, double vy, d
     r.atr = pm_atan2(omega * p.lr - vy, r.vx_eff);
     return r;
 }
-// The Pacejka sine as the sine of sincos: the lane-parallel chains of block_linearize evaluate
-// sincos for every lane (the phi lanes need the cosine), so the per-step kernels take the same value.
-__device__ __forceinline__ double tire_sin(double z) {
-    double s, c;
-    pm_sincos(z, &s, &c);
-    return s;
-}
+// The Pacejka sine (physics.h: pm_tire_sin, the same value on every path).
+__device__ __forceinline__ double tire_sin(double z) { return pm_tire_sin(z); }
 __device__ __forceinline__ double front_force(const VP& p, double atf, double delta) {
     const double alpha_f = clampd(-atf + delta, -p.maxAlpha, p.maxAlpha);
     return p.Df * tire_sin(p.Cf * pm_atan(p.Bf * alpha_f));
@@ -250,18 +245,21 @@ __global__ __launch_bounds__(256) void jac_kernel(const KArgs a) {
 // and jac_kernel's arithmetic for ONE instance and NT threads, with A_k, B_k, g_k written to LDS in the
 // stage records the solve kernel's condensing reads.  xs / us: the state and input (LDS).  Ends with a barrier.
 //
-// The rollout is a serial chain: per stage, atan2 -> atan -> sincos on three lanes.  The Jacobian
-// columns of stage k need the same chain at perturbed copies of x_k, known as soon as x_k is: lanes
-// 3 .. 21 run those evaluations IN THE SAME instruction stream as the rollout lanes (the stage's
-// latency does not change; round 1 ran them as a separate 29 k-cycle pass).  Lane roles, stage k:
-//   0 / 1 / 2   rollout: front tire, rear tire, pm_sincos(phi) at x_k (raw, rollout_kernel's form)
+// The rollout is a serial chain through the tire forces: per stage, atan2 -> atan -> the Pacejka sine on two lanes.
+// Only vx, vy and omega feed back (f_3..5 do not read X, Y or phi; phi_{k+1} = phi_k + Ts omega_k), so the chain
+// carries those and phi; sin / cos(phi_k) -- needed only for X, Y and the phi column -- are evaluated after it, for
+// all stages at once, and X_k, Y_k are then summed in the rollout's order.  The Jacobian columns of stage k need
+// the tire chain at perturbed copies of x_k, known as soon as x_k is: lanes 3 .. 18 run those evaluations IN THE
+// SAME instruction stream as the rollout lanes (the stage's latency does not change).  Lane roles, stage k:
+//   0 / 1       rollout: front tire, rear tire at x_k (raw, rollout_kernel's form)
 //   3 / 4       base front / rear tire at x_k + 0.0 (cheap_columns' t0)
 //   5 .. 16     4 lanes per state column (vx, vy, omega): (+eps front, +eps rear, -eps front, -eps rear)
 //   17 / 18     front tire at delta +- eps (the delta column)
-//   19 / 20     pm_sincos(phi +- eps) (the phi column);   21   pm_sincos(phi + 0.0)
-// Their sines go to tj[k][lane], the cosines of lanes 19 .. 21 to tj[k][0 .. 2].  An assembly pass (one
-// stage per lane) then forms f at each perturbed point with f_parts and the difference quotients:
-// the values state_column / cheap_columns compute (jac_kernel), bit for bit.
+// Their sines go to tj[k][lane].  The phi pass (after the chain), lane v N + k: sincos(phi_k + {-0.0, +eps, -eps}),
+// v = 0 / 1 / 2: sin / cos(phi_k + 0.0) -> tj[k][21] / tj[k][2] (sin(phi + 0.0) = sin(phi) + 0.0 exactly, cos is
+// even), sin / cos(phi_k +- eps) -> tj[k][19 / 20] / tj[k][0 / 1], and lane k forms the rollout's f_0, f_1 of stage
+// k from the raw sin / cos.  An assembly pass (one stage per lane) then forms f at each perturbed point with f_parts
+// and the difference quotients: the values state_column / cheap_columns compute (jac_kernel), bit for bit.
 constexpr int TJ = 24;
 // Layout: one record of LREC doubles per stage, rec + LREC k = [A_k 36 | B_k 12 | g_k 6] on exit.  While
 // the stage is being formed the same record holds its scratch: the tire / sincos evaluations at [0, TJ) and
@@ -278,18 +276,16 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
     const double eps = 1e-5;
     if (t < 64) {
         double x[6];
-        for (int i = 0; i < 6; ++i) x[i] = xs[i];
+        for (int i = 2; i < 6; ++i) x[i] = xs[i];
         const double u0 = us[0], u1 = us[1];
         double sd, cd;
         pm_sincos(u1, &sd, &cd);
-        // this lane's role (see above): tire chain or sincos, which tire, which input it perturbs
-        const bool roll = t < 3;
-        const bool tire = (t < 2) || (t >= 3 && t <= 18);
+        // this lane's role (see above): which tire, which input it perturbs
+        const bool roll = t < 2;
         const bool fr = (t == 0) || (t == 3) || (t >= 5 && t <= 16 && ((t - 5) & 1) == 0) || t == 17 || t == 18;
         const int col = (t >= 5 && t <= 16) ? (t - 5) >> 2 : -1;             // 0 vx, 1 vy, 2 omega
         const double sgn = (t >= 5 && t <= 16 && ((t - 5) & 2)) ? -eps : eps;
         const double dlt = (t == 17) ? u1 + eps : ((t == 18) ? u1 - eps : u1);
-        const double pz = (t == 19) ? eps : ((t == 20) ? -eps : 0.0);
         const double Bt = fr ? p.Bf : p.Br, Ct = fr ? p.Cf : p.Cr;
         // The roles as per-lane constants, so the stage body is one branch-free instruction stream: the
         // evaluation point is x_i + d_i with d_i = -0.0 on the rollout lanes (x + -0.0 = x for every x, -0.0
@@ -299,8 +295,8 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
         const double dvy = roll ? -0.0 : (col == 1 ? sgn : 0.0);
         const double dom = roll ? -0.0 : (col == 2 ? sgn : 0.0);
         const double Lt = fr ? p.lf : p.lr, sy = fr ? 1.0 : -1.0, sa = fr ? -1.0 : 1.0, dl = fr ? dlt : -0.0;
-        const double dz = (t == 2) ? -0.0 : pz;
-        const unsigned mtire = opaque_u(tire ? 0xffffffffu : 0u);
+        // lanes whose sine is used (the range check of the Pacejka sine's fast form looks at these only)
+        const unsigned long long used = 0x7fffbull;   // lanes 0, 1, 3 .. 18
         for (int k = 0; k < N; ++k) {
             const double phi = x[2], vx = x[3], vy = x[4], omega = x[5];
             // this lane's evaluation point (state_column / cheap_columns: x_i + 0.0, the column x_i +- eps)
@@ -310,28 +306,58 @@ __device__ __forceinline__ void block_linearize(const int t, const VP& p, int N,
             const double vx_eff = np_sign(vxl) * mx;
             const double at = pm_atan2(oml * Lt + sy * vyl, vx_eff);
             const double alpha = clampd(sa * at + dl, -p.maxAlpha, p.maxAlpha);
-            // tire lanes: Ct atan(Bt alpha); the sincos lanes: phi + dz (a bitwise select: no branch)
-            const double z = bitsel(mtire, Ct * pm_atan(Bt * alpha), phi + dz);
-            double sz, cz;
-            pm_sincos(z, &sz, &cz);
-            if (t >= 3 && t <= 21) tj[LREC * k + t] = sz;
-            if (t >= 19 && t <= 21) tj[LREC * k + t - 19] = cz;
+            const double z = Ct * pm_atan(Bt * alpha);
+            // pm_tire_sin per lane: the polynomial, or -- where a used lane's argument leaves its interval (other
+            // Params, NaN) -- the library sine on those lanes (a wave-uniform branch around it)
+            double sz = tire_sin_poly(z);
+            if (__ballot(!tire_sin_in_range(z)) & used) {
+                if (!tire_sin_in_range(z)) sz = pm_sin(z);
+            }
+            if (t >= 3 && t <= 18) tj[LREC * k + t] = sz;
             const double Fy_f = p.Df * readlane_d(sz, 0), Fy_r = p.Dr * readlane_d(sz, 1);
-            const double sphi = readlane_d(sz, 2), cphi = readlane_d(cz, 2);
             const double Frx = (p.Cm1 - p.Cm2 * vx) * u0 - p.Cr0 - p.Cr2 * (vx * vx);
             double f[6];
-            f[0] = vx * cphi - vy * sphi;
-            f[1] = vx * sphi + vy * cphi;
             f[2] = omega;
             f[3] = (1.0 / p.m) * (Frx - Fy_f * sd + p.m * vy * omega);
             f[4] = (1.0 / p.m) * (Fy_r + Fy_f * cd - p.m * vx * omega);
             f[5] = (1.0 / p.Iz) * (Fy_f * p.lf * cd - Fy_r * p.lr);
             if (t == 0)
-                for (int i = 0; i < 6; ++i) {
+                for (int i = 2; i < 6; ++i) {
                     xf[LREC * k + i] = x[i];
                     xf[LREC * k + 6 + i] = f[i];
                 }
-            for (int i = 0; i < 6; ++i) x[i] = x[i] + Ts * f[i];
+            for (int i = 2; i < 6; ++i) x[i] = x[i] + Ts * f[i];
+            (void)phi;
+        }
+    }
+    __syncthreads();
+    // the phi pass: lane v N + k, stage k, offset {-0.0, +eps, -eps}[v] (3 N <= 64 lanes per round)
+    for (int l = t; l < 3 * N; l += NT) {
+        const int v = l / N, k = l - v * N;
+        const double phik = xf[LREC * k + 2];
+        double sp, cp;
+        pm_sincos(phik + (v == 0 ? -0.0 : (v == 1 ? eps : -eps)), &sp, &cp);
+        double* const T = tj + LREC * k;
+        if (v == 0) {
+            T[21] = sp + 0.0;   // sin(phi + 0.0)
+            T[2] = cp;          // cos(phi + 0.0)
+            const double vx = xf[LREC * k + 3], vy = xf[LREC * k + 4];
+            xf[LREC * k + 6] = vx * cp - vy * sp;   // the rollout's f_0, f_1 at the raw phi_k
+            xf[LREC * k + 7] = vx * sp + vy * cp;
+        } else {
+            T[18 + v] = sp;     // 19: phi + eps, 20: phi - eps
+            T[v - 1] = cp;      // 0 / 1
+        }
+    }
+    __syncthreads();
+    // X_k, Y_k in the rollout's order: X_{k+1} = X_k + Ts f_0(x_k)
+    if (t == 0) {
+        double X = xs[0], Y = xs[1];
+        for (int k = 0; k < N; ++k) {
+            xf[LREC * k + 0] = X;
+            xf[LREC * k + 1] = Y;
+            X = X + Ts * xf[LREC * k + 6];
+            Y = Y + Ts * xf[LREC * k + 7];
         }
     }
     __syncthreads();

@@ -981,11 +981,13 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         typedef __attribute__((address_space(3))) volatile double* LdsVD;
         auto cold = [&](int i) -> double { return ((LdsVD)s_cold)[i * CS + t]; };
         // the unscaled bounds of rows t (as formed above from the configuration; exact-mode certificate)
+        // (both channels' values as scalar loads, then a select: a select of the two ADDRESSES is what the compiler
+        // forms otherwise -- a per-lane 64-bit address hoisted out of the solve and spilled)
         auto raw_bounds = [&](double& lb_, double& ub_, double& lr_, double& ur_) {
-            lb_ = ch ? c.u_lo[1] : c.u_lo[0];
-            ub_ = ch ? c.u_hi[1] : c.u_hi[0];
-            lr_ = ch ? c.du_lo[1] : c.du_lo[0];
-            ur_ = ch ? c.du_hi[1] : c.du_hi[0];
+            lb_ = ch ? uniformize(c.u_lo[1]) : uniformize(c.u_lo[0]);
+            ub_ = ch ? uniformize(c.u_hi[1]) : uniformize(c.u_hi[0]);
+            lr_ = ch ? uniformize(c.du_lo[1]) : uniformize(c.du_lo[0]);
+            ur_ = ch ? uniformize(c.du_hi[1]) : uniformize(c.du_hi[0]);
             if (kk == 0) { lr_ += s_up[ch]; ur_ += s_up[ch]; }
         };
         // scaled P to LDS (row stride PS)
@@ -1702,7 +1704,12 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 const double bb = actb < 0 ? slb : (actb > 0 ? sub : 0.0);
                 const double br = actr < 0 ? slr : (actr > 0 ? sur : 0.0);
                 double px_ = 0.0, pyb = 0.0, pyr = 0.0;
-                double r1 = -qi, r2b = actb ? bb : 0.0, r2r = actr ? br : 0.0;
+                // (-q through an opaque copy formed here: hoisted out of the phase loop, the negated q was live
+                // across the whole solve and spilled)
+                double nqi = qi;
+                asm volatile("" : "+v"(nqi));
+                nqi = -nqi;
+                double r1 = nqi, r2b = actb ? bb : 0.0, r2r = actr ? br : 0.0;
                 double axb = 0.0, axr = 0.0;
                 for (int rf = 0; rf <= c.polish_refine_iter; ++rf) {
                     double tv = Kmul(r1 + ATw(actb ? cdiv(r2b, dl, dlinv) : 0.0, actr ? cdiv(r2r, dl, dlinv) : 0.0));
@@ -1714,7 +1721,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     if (rf == c.polish_refine_iter) break;
                     double Pxv = Pmul(px_);
                     double atyv = ATw(pyb, pyr);
-                    r1 = -qi - Pxv - atyv;
+                    r1 = nqi - Pxv - atyv;
                     Ax(px_, axb, axr);
                     r2b = actb ? bb - axb : 0.0;
                     r2r = actr ? br - axr : 0.0;
