@@ -96,11 +96,16 @@ typedef struct {
 
 /* Horizon tiers (mpc_step takes any N, mpc_6stati.py:125):
  *   N <= TRAJ_MAX_N (40)                 the register-resident hot kernels (mpc_solve.h): every entry point;
- *   TRAJ_MAX_N < N <= TRAJ_MAX_N_GENERAL the general condensed-QP solver (mpc_general.h, one 256-thread workgroup
- *                                        per instance, its Cholesky factor in the caller's scratch): the step and
- *                                        QP entry points only (traj_mpc_step_batch / traj_mpc_qp_batch); the
- *                                        closed-loop entry points return TRAJ_E_UNSUPPORTED. */
+ *   TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG    without state bounds: the long-horizon kernel (mpc_long.h: the hot kernels'
+ *                                        algorithm with one thread per QP variable, K^-1 in LDS up to N = 64 and in
+ *                                        the caller's scratch beyond);
+ *   otherwise (state bounds, or N > TRAJ_MAX_N_LONG up to TRAJ_MAX_N_GENERAL) the general condensed-QP solver
+ *                                        (mpc_general.h, one 256-thread workgroup per instance, its Cholesky factor
+ *                                        in the caller's scratch).
+ * Past TRAJ_MAX_N only the step and QP entry points run (traj_mpc_step_batch / traj_mpc_qp_batch, the scratch of
+ * traj_mpc_sb_workspace_bytes); the closed-loop entry points return TRAJ_E_UNSUPPORTED. */
 #define TRAJ_MAX_N 40
+#define TRAJ_MAX_N_LONG 128
 #define TRAJ_MAX_N_GENERAL 256
 
 int traj_abi_version(void);
@@ -133,8 +138,8 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
  * step t = 0 starts cold. */
 size_t traj_mpc_workspace_bytes(int B, int N);
 /* Scratch of the general solver, which runs with state bounds (x_lo / x_hi given with a finite side,
- * mpc_6stati.py:208-213) and for every horizon N > TRAJ_MAX_N: B * ~20.5k doubles at N = 20 (N > TRAJ_MAX_N adds
- * the Cholesky factor, 4 N^2 doubles).  traj_mpc_step_batch then needs traj_mpc_workspace_bytes(B, N) + this many
+ * mpc_6stati.py:208-213), and of the long-horizon kernel (every horizon N > TRAJ_MAX_N): B * ~20.5k doubles at
+ * N = 20 (N > TRAJ_MAX_N adds the Cholesky factor, 4 N^2 doubles; the long-horizon kernel uses at most 8 N^2 + 112 N).  traj_mpc_step_batch then needs traj_mpc_workspace_bytes(B, N) + this many
  * bytes; traj_mpc_qp_batch this many.  0 for B < 0 or N outside 1 .. TRAJ_MAX_N_GENERAL. */
 size_t traj_mpc_sb_workspace_bytes(int B, int N);
 

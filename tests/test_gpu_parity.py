@@ -528,13 +528,15 @@ def test_dropin_mpc_step_contract(gpu, oracle_lib):
     assert not np.array_equal(i6["U_opt"], info["U_opt"])
 
 
-@pytest.mark.parametrize("N,Ts,B", [(60, 0.02, 24), (41, 0.05, 16), (60, 0.05, 16)])
+@pytest.mark.parametrize("N,Ts,B", [(60, 0.02, 24), (41, 0.05, 16), (60, 0.05, 16), (64, 0.02, 12), (65, 0.02, 8),
+                                    (128, 0.02, 4)])
 def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
-    """Horizons past the hot kernels' capacity (TRAJ_MAX_N = 40) run the general condensed-QP solver with its
-    Cholesky factor in the caller's scratch (include/trajmpc.h horizon tiers): mpc_step takes any N
-    (mpc_6stati.py:125).  Batch entry point and the drop-in module against the oracle at the step tests' bars:
-    statuses identical, iteration counts equal on >= 95 %, U within 1e-6 where both polished and 1e-4 where
-    neither did; the drop-in returns the batch's u_cmd and the reference's fallback contract."""
+    """Horizons past the hot kernels' capacity (TRAJ_MAX_N = 40) run the long-horizon kernel (mpc_long.h: the hot
+    algorithm with one thread per variable, K^-1 in LDS up to N = 64, in the caller's scratch from N = 65 to
+    TRAJ_MAX_N_LONG = 128; include/trajmpc.h horizon tiers): mpc_step takes any N (mpc_6stati.py:125).  Batch entry
+    point and the drop-in module against the oracle at the step tests' bars: statuses identical, iteration counts
+    equal on >= 95 %, U within 1e-6 where both polished and 1e-4 where neither did; the drop-in returns the batch's
+    u_cmd and the reference's fallback contract."""
     from trajectory_generation_amd import mpc_6stati as M
     g, r = _step_both(oracle_lib, 17, B, N, Ts, 0)
     assert np.array_equal(g["status"], r["status"])
@@ -580,6 +582,24 @@ def test_step_in_kernel_linearization_bit_identical(gpu, N, Ts):
     for k in outs[0]:
         a, b = outs[1][k], outs[0][k]
         assert bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) if a.is_floating_point() else torch.equal(a, b), k
+
+
+@pytest.mark.parametrize("N,B", [(65, 3), (130, 2)])
+def test_general_solver_past_128_variables_vs_oracle(gpu, oracle_lib, N, B):
+    """The general solver (state bounds, mpc_general.h) past n = 128 variables, where its one-wave triangular solves
+    hold three or more rows per lane and the Cholesky factor lives in the caller's scratch: statuses, iteration
+    counts and polish outcomes identical to the oracle, U within 1e-6 where both polished (Ts = 0.02, speed band)."""
+    x_lo, x_hi = SB["vx"]
+    g, r = _sb_both(oracle_lib, 29, B, N, 0.02, 0, x_lo, x_hi)
+    assert np.array_equal(g["status"], r["status"])
+    assert np.array_equal(g["iters"], r["iters"])
+    pg, pr = g["polished"] > 0, r["polished"] > 0
+    assert np.array_equal(pg, pr)
+    ok = g["status"] <= 1
+    assert ok.any()
+    du = np.abs(g["U_opt"] - r["U_opt"]).max(axis=(1, 2))
+    assert du[pg & pr & ok].max(initial=0.0) <= 1e-6
+    assert du[~pg & ~pr & ok].max(initial=0.0) <= 1e-4
 
 
 def _lib_status(code):

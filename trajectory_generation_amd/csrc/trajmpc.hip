@@ -13,6 +13,7 @@
 #include "../../include/trajmpc.h"
 #include "mpc_common.h"
 #include "mpc_general.h"
+#include "mpc_long.h"
 #include "mpc_linearize.h"
 #include "physics.h"
 
@@ -160,7 +161,14 @@ __global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, 
 // ---------------------------------------------------------------- MPC dispatch
 
 // per-capacity launchers (mpc_inst.hip compiled once per NN)
+#ifndef TGMPC_CAP64
+#define TGMPC_CAP64 1   // capacity 64 (one wave) for 20 < N <= 32; 0: those horizons run the capacity-80 kernel
+#endif
+#if TGMPC_CAP64
 #define TGMPC_CAPACITIES(X) X(16) X(32) X(40) X(64) X(80)
+#else
+#define TGMPC_CAPACITIES(X) X(16) X(32) X(40) X(80)
+#endif
 #define TGMPC_DECL(NNV) int launch_mpc_##NNV(const KArgs& a, hipStream_t st, int mode);
 TGMPC_CAPACITIES(TGMPC_DECL)
 #undef TGMPC_DECL
@@ -222,6 +230,28 @@ static int check_cfg(const traj_mpc_config* c, bool allow_sb = false) {
 static int launch_general(const KArgs& a, double* gws, hipStream_t st) {
     const size_t per = gen_ws_doubles(a.c.N);
     hipLaunchKernelGGL(solve_gen_kernel, dim3(a.B), dim3(GEN_NT), 0, st, a, gws, per);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+// the long-horizon kernel (mpc_long.h): TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG without state bounds; its per-instance
+// scratch (the scaled P, and K^-1 past LONG_NKL) is the caller's, in the same region as the general solver's
+static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
+    const int N = a.c.N;
+    const size_t per = long_ws_doubles(N);
+    if (2 * N <= LONG_NKL) {
+        const size_t lds = long_lds_bytes(N);
+        static bool attr = false;   // (per process: the attribute is a property of the function)
+        if (!attr) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_long_kernel<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(LONG_NKL * LONG_NKL * sizeof(double))) != hipSuccess)
+                return TRAJ_E_LAUNCH;
+            attr = true;
+        }
+        hipLaunchKernelGGL(solve_long_kernel<true>, dim3(a.B), dim3(LONG_NT), lds, st, a, lws, per);
+    } else {
+        hipLaunchKernelGGL(solve_long_kernel<false>, dim3(a.B), dim3(LONG_NT), 0, st, a, lws, per);
+    }
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
@@ -472,7 +502,11 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     // the step: one launch with the linearization in the workgroup (mode 4), or rollout_kernel + jac_kernel +
     // the solve (traj_debug_step_linearize(0); the general solver always reads A/B/g from the workspace)
     if (lin && (sb || !g_step_inlin)) launch_linearize(a, (hipStream_t)stream, false);
-    if (sb) return launch_general(a, (double*)((char*)ws + base), (hipStream_t)stream);
+    if (sb) {
+        double* const sws = (double*)((char*)ws + base);
+        if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long(a, sws, (hipStream_t)stream);
+        return launch_general(a, sws, (hipStream_t)stream);
+    }
     return launch_mpc(a, (hipStream_t)stream, lin ? (g_step_inlin ? 4 : 0) : 1);
 }
 
