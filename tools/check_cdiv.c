@@ -1,6 +1,7 @@
 /* cdiv (trajectory_generation_amd/csrc/mpc_common.h) against IEEE division on the build host: d / c as
  * q = d y, t = q c - d (fma), q - t y (fma), y = 1 / c rounded.  Random operands over the whole normal range plus
- * signed zeros and subnormals; prints mismatches per divisor (exit 1 if any has |d| >= 1e-290).
+ * signed zeros and subnormals; prints mismatches per divisor (exit 1 if any has |d| >= 1e-290); then the non-finite
+ * operands and overflowing quotients, where cdiv is NaN and IEEE +-inf (exit 1 if either side is finite).
  *   gcc -O2 -o /tmp/check_cdiv tools/check_cdiv.c -lm && /tmp/check_cdiv */
 #include <math.h>
 #include <stdint.h>
@@ -51,6 +52,17 @@ int main(void) {
                "mismatch %.3g\n", c, n, bad, bad_sub, dmax);
         if (dmax < 1e-290) bad = 0;   /* remainder underflow only: |d| below 1e-290 */
         total_bad_normal += bad;
+    }
+    /* non-finite operands and overflowing quotients (documented in mpc_common.h): the remainder is inf - inf, so cdiv
+     * gives NaN where IEEE gives +-inf -- both non-finite (the solver's finiteness check rejects either); NaN stays NaN */
+    {
+        const double c = 2.0 * 1e-5, y = 1.0 / c;
+        const double nf[] = {INFINITY, -INFINITY, NAN, 1.7e308, -1.7e308};
+        for (int k = 0; k < 5; ++k) {
+            const double q = cdiv(nf[k], c, y), ref = nf[k] / c;
+            printf("d = %g: cdiv %g, IEEE %g\n", nf[k], q, ref);
+            if (isfinite(q) || isfinite(ref)) total_bad_normal += 1;   /* never a finite result on one side only */
+        }
     }
     return total_bad_normal ? 1 : 0;
 }

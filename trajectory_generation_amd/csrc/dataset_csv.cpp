@@ -19,6 +19,7 @@
 #include <memory>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -99,7 +100,7 @@ extern "C" {
 int traj_dataset_write_csv(const char* clean_path, const char* noisy_path, int B, int T, double Ts,
                            const double* X, const double* U, const double* noise, const long long* ids,
                            int nthreads) {
-    if (B < 0 || T < 0 || (!clean_path && !noisy_path) || (B > 0 && (!X || !U || !ids))) return TRAJ_E_ARG;
+    if (B < 0 || T < 0 || (!clean_path && !noisy_path) || (B > 0 && (!X || (T > 0 && !U) || !ids))) return TRAJ_E_ARG;
     if (noisy_path && B > 0 && !noise) return TRAJ_E_ARG;
     const int R = T + 1;   // rows per trajectory
     for (int which = 0; which < 2; ++which) {
@@ -229,7 +230,12 @@ int traj_dataset_read_csv(const char* path, long long rows, int ncols, double* o
                     o[c] = NAN;
                 } else {
                     auto res = std::from_chars(s, e, o[c]);
-                    if (res.ec != std::errc() || res.ptr != e) {
+                    if (res.ec == std::errc::result_out_of_range && res.ptr == e) {
+                        // a literal past the double range: the value Python's float() / pandas give it (+-inf, or a
+                        // signed zero / the nearest subnormal), from strtod on the token
+                        std::string tok(s, e);
+                        o[c] = std::strtod(tok.c_str(), nullptr);
+                    } else if (res.ec != std::errc() || res.ptr != e) {
                         // "nan" / "inf" spellings pandas may write
                         std::string tok(s, e);
                         if (tok == "nan" || tok == "NaN") o[c] = NAN;

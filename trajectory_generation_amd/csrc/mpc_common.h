@@ -181,7 +181,10 @@ __device__ __forceinline__ double vmin(double a, double b) {
 }
 // The ADMM projection onto [lo, hi] (lo <= hi) as v_max_f64 + v_min_f64: 2 VALU instead of two compares and four
 // selects.  Equal to clampd for every non-NaN x up to the sign of a zero against a zero bound; a NaN maps to lo,
-// as OSQP's own project() (c_min(c_max(z, l), u)) maps it, where clampd and the oracle pass the NaN through.
+// as OSQP's own project() (c_min(c_max(z, l), u)) maps it, where clampd and the oracle pass the NaN through.  A NaN
+// iterate needs NaN data (rejected before the ADMM, "Solver Error" on both sides) or an overflow inside the ADMM; the
+// dual update y += rho (z~ - z) then carries the NaN on both sides, every residual is NaN, no termination test
+// passes, and both end at max_iter with the same status.
 __device__ __forceinline__ double clamp_mm(double x, double lo, double hi) { return vmin(vmax(x, lo), hi); }
 __device__ __forceinline__ double vmax_abs(double a, double b) {
     double r;
@@ -236,9 +239,12 @@ __device__ __forceinline__ double rcp_n(double b) {
 }
 
 // d / c for a constant c with y = 1 / c (rounded) given: q = d y corrected once by the exact remainder
-// (Markstein): r = -(q c - d) by fma, q + r y -- the IEEE quotient bit for bit for d = +-0 and every |d| >= 1e-290
-// (tools/check_cdiv.c: random operands over the whole exponent range for c = 2e-5, 1e-6 and every even 2..512; below
-// that the remainder underflows and the last bit can differ), in 3 f64 operations instead of ~10.  Used for the
+// (Markstein): r = -(q c - d) by fma, q + r y -- the IEEE quotient bit for bit for d = +-0 and every FINITE d with
+// |d| >= 1e-290 whose quotient does not overflow (tools/check_cdiv.c: random operands over the whole exponent range
+// for c = 2e-5, 1e-6 and every even 2..512; below 1e-290 the remainder underflows and the last bit can differ).  For
+// d = +-inf, or a quotient past DBL_MAX, the remainder is inf - inf and the result NaN where IEEE gives +-inf: a
+// non-finite either way, and every caller's data then fails the solver's finiteness check (status "Solver Error",
+// as the oracle's +-inf does), so the statuses agree.  3 f64 operations instead of ~10.  Used for the
 // central differences' (fp - fm) / (2 eps) on every path (the fused and per-step linearizations agree), the
 // polish's quotients by delta and the Ruiz mean's by n.
 __device__ __forceinline__ double cdiv(double d, double c, double y) {

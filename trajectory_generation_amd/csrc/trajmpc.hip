@@ -277,7 +277,9 @@ static int g_fused_grid = 0;        // traj_debug_fused_grid
 static int g_fused_waves = 0;       // traj_debug_fused_waves: 0 = by launch length, 2 or 3 = forced
 static int g_spin_limit = 1 << 22;  // traj_debug_spin_limit: polls before a fused hand-off is declared lost
 static int g_lead_steps = TGMPC_LEAD_STEPS, g_lead_permille = TGMPC_LEAD_PERMILLE;   // traj_debug_queue_lead
-static int g_step_inlin = 1;        // traj_debug_step_linearize: the step's linearization inside the solve launch
+// traj_debug_step_linearize: the step's linearization inside the solve launch.  An atomic: a test that flips it may run
+// beside other callers of the library; each traj_mpc_step_batch reads it once.
+static std::atomic<int> g_step_inlin{1};
 
 // per-kernel timing of traj_closed_loop_step (traj_debug_kernel_timing): 5 events per step bracket
 // rollout | jac | order | solve on the launch stream
@@ -328,7 +330,7 @@ int traj_debug_queue_lead(int steps, int per_mille) {
 
 int traj_debug_step_linearize(int in_kernel) {
     if (in_kernel != 0 && in_kernel != 1) return TRAJ_E_ARG;
-    g_step_inlin = in_kernel;
+    g_step_inlin.store(in_kernel, std::memory_order_relaxed);
     return TRAJ_OK;
 }
 
@@ -501,13 +503,14 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     a.dbg = g_dbg;
     // the step: one launch with the linearization in the workgroup (mode 4), or rollout_kernel + jac_kernel +
     // the solve (traj_debug_step_linearize(0); the general solver always reads A/B/g from the workspace)
-    if (lin && (sb || !g_step_inlin)) launch_linearize(a, (hipStream_t)stream, false);
+    const int inlin = g_step_inlin.load(std::memory_order_relaxed);
+    if (lin && (sb || !inlin)) launch_linearize(a, (hipStream_t)stream, false);
     if (sb) {
         double* const sws = (double*)((char*)ws + base);
         if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long(a, sws, (hipStream_t)stream);
         return launch_general(a, sws, (hipStream_t)stream);
     }
-    return launch_mpc(a, (hipStream_t)stream, lin ? (g_step_inlin ? 4 : 0) : 1);
+    return launch_mpc(a, (hipStream_t)stream, lin ? (inlin ? 4 : 0) : 1);
 }
 
 // A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order
