@@ -139,7 +139,7 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
 size_t traj_mpc_workspace_bytes(int B, int N);
 /* Scratch of the general solver, which runs with state bounds (x_lo / x_hi given with a finite side,
  * mpc_6stati.py:208-213), and of the long-horizon kernel (every horizon N > TRAJ_MAX_N): B * ~20.5k doubles at
- * N = 20 (N > TRAJ_MAX_N adds the Cholesky factor, 4 N^2 doubles; the long-horizon kernel uses at most 8 N^2 + 112 N).  traj_mpc_step_batch then needs traj_mpc_workspace_bytes(B, N) + this many
+ * N = 20 (N > TRAJ_MAX_N adds the Cholesky factor, 4 N^2 doubles; the long-horizon kernel uses at most 2 (2N + 6)^2).  traj_mpc_step_batch then needs traj_mpc_workspace_bytes(B, N) + this many
  * bytes; traj_mpc_qp_batch this many.  0 for B < 0 or N outside 1 .. TRAJ_MAX_N_GENERAL. */
 size_t traj_mpc_sb_workspace_bytes(int B, int N);
 

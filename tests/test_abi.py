@@ -136,15 +136,15 @@ def test_state_bound_workspace_bytes(L):
 
 def test_long_horizon_scratch_fits_the_state_bound_region():
     """The long-horizon kernel (mpc_long.h, TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG) takes its scratch from the same
-    caller-owned region: the scaled P column-major with leading dimension ld = n rounded up to 8, and K^-1 beside
-    it past n = 128 (below, K^-1 is in LDS) -- never more than traj_mpc_sb_workspace_bytes gives per instance."""
+    caller-owned region: the scaled P, ld x ld column-major with ld = n rounded up to 8, and K^-1 beside it past
+    n = 128 (below, K^-1 is in LDS) -- never more than traj_mpc_sb_workspace_bytes gives per instance."""
     def gen(N):
         n, m = 2 * N, 10 * N
         return n * n + m * n + 6 * (N + 1) * n + 6 * (N + 1) + 3 * n + 20 * n + 24 * m + 64 + n * n
     for N in range(_lib.MAX_N + 1, _lib.MAX_N_LONG + 1):
         n = 2 * N
         ld = (n + 7) // 8 * 8
-        assert ld * n * (2 if n > 128 else 1) <= gen(N), N
+        assert ld * ld * (2 if n > 128 else 1) <= gen(N), N
     assert _lib.MAX_N < _lib.MAX_N_LONG <= _lib.MAX_N_GENERAL
 
 

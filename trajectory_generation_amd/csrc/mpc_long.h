@@ -11,10 +11,13 @@
 //   * K = P + sigma I + A' diag(rho) A is inverted explicitly by the symmetric sweep operator (n pivots), so every
 //     ADMM iteration is one dense mat-vec -- as in the hot kernel.
 // Layout: one 256-thread workgroup per instance, thread t owns variable t (n <= 256).  The scaled P lives in the
-// caller's scratch, COLUMN-major (entry (r, j) at j ld + r: for fixed j the threads read consecutive doubles);
-// K^-1 the same way, in LDS (dynamic shared memory, n <= LONG_NKL: 128 KB at n = 128) or in the scratch beyond.
-// A pivot of the sweep, a mat-vec, a Ruiz pass each stream the matrix once through the workgroup; the vectors
-// (broadcasts, +-2 exchanges, block maxima) go through small LDS buffers.
+// caller's scratch, COLUMN-major (entry (r, j) at j ld + r: for fixed j the threads read consecutive doubles), ld x ld
+// with ld = n rounded up to 8 and zero padding; K^-1 the same way, in LDS (dynamic shared memory, n <= LONG_NKL:
+// 128 KB at n = 128) or in the scratch beyond.  A pivot of the sweep, a mat-vec, a Ruiz pass each stream the
+// matrix once through the workgroup, 8 columns at a time with the next 8 loaded before this 8 are stored (a row
+// update is a read-modify-write whose columns the compiler cannot prove distinct, so without the explicit pipeline
+// every load waits for the previous store); the vectors (broadcasts, +-2 exchanges, block maxima) go through small
+// LDS buffers.
 #pragma once
 #include "mpc_common.h"
 
@@ -27,11 +30,11 @@ __host__ __device__ inline int long_ld(int n) { return (n + 7) & ~7; }
 // per-instance scratch (doubles): P, and K^-1 when it does not fit LDS
 __host__ __device__ inline size_t long_ws_doubles(int N) {
     const int n = 2 * N, ld = long_ld(n);
-    return (size_t)ld * n * (n > LONG_NKL ? 2 : 1);
+    return (size_t)ld * ld * (n > LONG_NKL ? 2 : 1);
 }
 __host__ inline size_t long_lds_bytes(int N) {
     const int n = 2 * N;
-    return n <= LONG_NKL ? (size_t)long_ld(n) * n * sizeof(double) : 0;
+    return n <= LONG_NKL ? (size_t)long_ld(n) * long_ld(n) * sizeof(double) : 0;
 }
 
 template <bool KL>
@@ -51,12 +54,52 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
     const bool own = t < n;
     const int kk = t >> 1, ch = t & 1;
     double* const P = lws + (size_t)b * lstride;                    // [j ld + r]
-    double* const Kg = P + (size_t)ld * n;                           // K^-1 in the scratch (!KL)
+    double* const Kg = P + (size_t)ld * ld;                          // K^-1 in the scratch (!KL)
     auto Kat = [&](int j) -> double& {
         if constexpr (KL) return s_kl[j * ld + t];
         else return Kg[(size_t)j * ld + t];
     };
     auto Pat = [&](int j) -> double& { return P[(size_t)j * ld + t]; };
+    // row t of a matrix (K or P), columns [0, jend) (jend a multiple of 8): v[j] <- f(j, v[j]), 8 columns at a time,
+    // the next chunk loaded before this one is stored
+    auto row_map = [&](auto&& at, int jend, auto&& f) {
+        double cur[8], nxt[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = at(i);
+        for (int j0 = 0; j0 < jend; j0 += 8) {
+            if (j0 + 8 < jend) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) nxt[i] = at(j0 + 8 + i);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) at(j0 + i) = f(j0 + i, cur[i]);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+        }
+    };
+    // sum_j row_t[j] v[j] (4 chains, the hot kernel's Kmul order) and max_j |row_t[j]|, 8 columns at a time
+    auto row_dot = [&](auto&& at, const double* v) -> double {
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int j0 = 0; j0 < ld; j0 += 8) {
+            double kv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kv[i] = at(j0 + i);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s4[i & 3] = fma(kv[i], v[j0 + i], s4[i & 3]);
+        }
+        return (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    };
+    auto row_absmax = [&](auto&& at) -> double {
+        double m = 0.0;
+        for (int j0 = 0; j0 < ld; j0 += 8) {
+            double kv[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) kv[i] = at(j0 + i);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) m = fmax(m, fabs(kv[i]));
+        }
+        return m;
+    };
     const double* x0 = a.x0 + 6 * (size_t)b;
     const double* up = a.u_prev + 2 * (size_t)b;
     const double* pref = a.path_ref + (size_t)3 * (N + 1) * b;
@@ -133,7 +176,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
     for (int i = 0; i < 6; ++i) xh[i] = x0[i];
     double qi = 0.0;
     if (own)
-        for (int j = 0; j < n; ++j) Pat(j) = 0.0;
+        for (int j = 0; j < ld; ++j) Pat(j) = 0.0;
     for (int k = 0; k < N; ++k) {
         const double* Ak = gA + 36 * k;
         double xn[6], Gn[6];
@@ -157,10 +200,13 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
         s_F[0][t] = F0; s_F[1][t] = F1; s_F[2][t] = F2;
         __syncthreads();
-        // F_k's columns >= 2 (k + 1) are zero (the inputs of later stages): row t's entries j < 2 k + 2 only
+        // F_k's columns >= 2 (k + 1) are zero (the inputs of later stages): row t's entries j < 2 k + 2 only (to the
+        // next multiple of 8; threads >= n hold F = 0, so the padding columns stay zero)
         if (own) {
             const int jm = 2 * k + 2 < n ? 2 * k + 2 : n;
-            for (int j = 0; j < jm; ++j) Pat(j) = fma(F0, s_F[0][j], fma(F1, s_F[1][j], fma(F2, s_F[2][j], Pat(j))));
+            row_map(Pat, (jm + 7) & ~7, [&](int j, double v) {
+                return fma(F0, s_F[0][j], fma(F1, s_F[1][j], fma(F2, s_F[2][j], v)));
+            });
         }
         __syncthreads();
     }
@@ -191,7 +237,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         int bad = 0;
         if (own) {
             bad |= !isfinite(qi);
-            for (int j = 0; j < n; ++j) bad |= !isfinite(Pat(j));
+            bad |= !isfinite(row_absmax(Pat));
         }
         if (bad) s_flag[0] = 1;
     }
@@ -218,7 +264,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         // ---- Ruiz equilibration + cost scaling (OSQP scale_data), as mpc_solve.h ----
         double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0, cn = 0.0;
         if (own)
-            for (int j = 0; j < n; ++j) cn = fmax(cn, fabs(Pat(j)));
+            cn = row_absmax(Pat);
         for (int it = 0; it < c.scaling_iters; ++it) {
             const double Er_up = exch(Er, +2), D_dn = exch(D, -2);
             const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
@@ -230,11 +276,11 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
             const double* dv = bcast(Dt);
             cn = 0.0;
             if (own)
-                for (int j = 0; j < n; ++j) {
-                    const double v = Pat(j) * (Dt * dv[j]);
-                    Pat(j) = v;
-                    cn = fmax(cn, fabs(v));
-                }
+                row_map(Pat, ld, [&](int j, double v) {
+                    const double w = v * (Dt * dv[j]);
+                    cn = fmax(cn, fabs(w));
+                    return w;
+                });
             qi *= Dt;
             D *= Dt;
             Eb *= Etb;
@@ -246,8 +292,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
             ct = 1.0 / limit_scaling(ct);
             cs *= ct;
         }
-        if (own)
-            for (int j = 0; j < n; ++j) Pat(j) *= cs;
+        if (own) row_map(Pat, ld, [&](int, double v) { return v * cs; });
         qi *= cs;
         const double csinv = 1.0 / cs;
         const double D_dn = exch(D, -2);
@@ -270,17 +315,11 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         };
         auto Pmul = [&](double v) -> double {   // (P v)_t, P symmetric: row t = column t
             const double* vb = bcast(v);
-            double s4[4] = {0.0, 0.0, 0.0, 0.0};
-            if (own)
-                for (int j = 0; j < n; ++j) s4[j & 3] = fma(Pat(j), vb[j], s4[j & 3]);
-            return own ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0;
+            return own ? row_dot(Pat, vb) : 0.0;
         };
         auto Kmul = [&](double v) -> double {   // (K^-1 v)_t
             const double* vb = bcast(v);
-            double s4[4] = {0.0, 0.0, 0.0, 0.0};
-            if (own)
-                for (int j = 0; j < n; ++j) s4[j & 3] = fma(Kat(j), vb[j], s4[j & 3]);
-            return own ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0;
+            return own ? row_dot(Kat, vb) : 0.0;
         };
         auto rho_for = [&](double l, double u, double rho) -> double {
             if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
@@ -336,18 +375,25 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
                 const double dp = -kr_up * a_r_up * a_rp;          // (t, t+2)
                 const double dm = -kr * a_r * a_rm;                // (t, t-2): thread t-2's dp, the same product
                 if (own)
-                    for (int j = 0; j < n; ++j) {
-                        double v = Pat(j);
-                        v = (j == t) ? v + dii : v;
-                        v = (j == t + 2) ? v + dp : v;
-                        v = (j == t - 2 && has_prev) ? v + dm : v;
-                        Kat(j) = v;
+                    for (int j0 = 0; j0 < ld; j0 += 8) {
+                        double v[8];
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) v[i] = Pat(j0 + i);
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const int j = j0 + i;
+                            double w = v[i];
+                            w = (j == t) ? w + dii : w;
+                            w = (j == t + 2) ? w + dp : w;
+                            w = (j == t - 2 && has_prev) ? w + dm : w;
+                            Kat(j) = w;
+                        }
                     }
             }
             bool ok = true;
             for (int pv = 0; pv < n; ++pv) {
                 __syncthreads();
-                if (own) s_pc[t] = Kat(pv);
+                s_pc[t] = own ? Kat(pv) : 0.0;   // (rows >= n: zero, so the padding columns stay zero)
                 __syncthreads();
                 const double d = s_pc[pv];
                 ok = ok && (d > 0.0);
@@ -357,13 +403,12 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
                     const double fd = s_pc[t] * dinv;
                     const double be = piv ? dinv : -fd;
                     const double al = piv ? 0.0 : 1.0;
-                    for (int j = 0; j < n; ++j) Kat(j) = fma(be, s_pc[j], al * Kat(j));
+                    row_map(Kat, ld, [&](int j, double v) { return fma(be, s_pc[j], al * v); });
                     Kat(pv) = piv ? -dinv : fd;
                 }
             }
             __syncthreads();
-            if (own)
-                for (int j = 0; j < n; ++j) Kat(j) = -Kat(j);
+            if (own) row_map(Kat, ld, [&](int, double v) { return -v; });
             __syncthreads();
             if (!ok) {
                 if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
