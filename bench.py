@@ -54,7 +54,7 @@ def algorithmic_bytes_per_traj(N: int, kmax: int) -> int:
 
 def _capacity(n: int) -> int:
     """solve_kernel instance the library launches for 2N QP variables (trajmpc.hip launch_mpc)."""
-    return next(c for c in (16, 32, 40, 64, 80) if n <= c)
+    return next(c for c in (16, 32, 40, 80) if n <= c)
 
 
 def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):

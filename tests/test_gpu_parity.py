@@ -358,7 +358,7 @@ def test_closed_loop_history_matches_single_steps(gpu):
 def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
     """traj_closed_loop_run (one launch, in-workgroup linearization, on-chip state) equals the per-step
     launches bit for bit: histories, statuses, iteration counts; also when split into two runs.  Every
-    capacity the compact fused image covers: 16 (N 8), 32 (N 12), 40 (N 20), 64 (N 30), 80 (N 40)."""
+    capacity: 16 (N 8), 32 (N 12), 40 (N 20), 80 (N 30 and N 40: 20 < N <= 40 runs the two-wave instance)."""
     from trajectory_generation_amd.workload import make_workload
     Ts, T, B = 0.05, 24, 96
     w = make_workload(B, N, Ts, kind="mixed" if N == 40 else "spline", seed=6)
@@ -568,7 +568,7 @@ def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
 def test_step_in_kernel_linearization_bit_identical(gpu, N, Ts):
     """traj_mpc_step_batch runs the linearization inside the solve launch (one launch per call, block_linearize's
     stage records copied to the workspace for X_opt); it equals the rollout_kernel + jac_kernel + solve sequence bit
-    for bit in every output, at every kernel capacity (16, 40, 64, 80)."""
+    for bit in every output, at every kernel capacity (16, 40, 80: N 30 and 40)."""
     from trajectory_generation_amd import _lib
     x0, up, pr, vr = random_instances(23, 48, N, Ts)
     cfg = TB.config_struct(N=N, Ts=Ts)

@@ -161,8 +161,13 @@ __global__ __launch_bounds__(1024) void order_kernel(const double* warm, int B, 
 // ---------------------------------------------------------------- MPC dispatch
 
 // per-capacity launchers (mpc_inst.hip compiled once per NN)
+// Kernel capacities (QP variables, n = 2N): 16 / 32 / 40 one wave per instance, 80 two waves.  20 < N <= 40 runs
+// capacity 80: a one-wave capacity-64 instance has no spare lanes for the receiver sweep and, at 64 doubles of K^-1
+// per lane beside the chunked reads, spilled 780-830 B/lane at 512 registers; measured at B = 1024
+// (profiles/r05_tiers.json) it ran N = 24 / 30 / 32 at 0.43 / 0.34 / 0.35 M steps/s against 0.56 / 0.47 / 0.46 M on
+// capacity 80, so it is not built (TGMPC_CAP64=1 brings it back for experiments)
 #ifndef TGMPC_CAP64
-#define TGMPC_CAP64 1   // capacity 64 (one wave) for 20 < N <= 32; 0: those horizons run the capacity-80 kernel
+#define TGMPC_CAP64 0
 #endif
 #if TGMPC_CAP64
 #define TGMPC_CAPACITIES(X) X(16) X(32) X(40) X(64) X(80)
