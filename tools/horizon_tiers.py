@@ -1,5 +1,7 @@
-"""Horizon tiers: per-step batch throughput of traj_mpc_step_batch at B = 1024 (random spline
-windows, dt = 0.05) for horizons in each kernel tier, and the drop-in mpc_step per-call time.  Prints JSON."""
+"""Horizon tiers (include/trajmpc.h): per-step batch throughput of traj_mpc_step_batch at B = 1024
+(random parabola windows, dt = 0.05) for horizons in each kernel tier (one wave N <= 20, two waves 20 < N <= 40, the
+long-horizon kernel 40 < N <= 128), and the drop-in mpc_step per-call time (median of 20).  One JSON line per N.
+  python tools/horizon_tiers.py [N,N,...]"""
 import json
 import sys
 import time
@@ -27,7 +29,7 @@ def instances(B, N, Ts, seed=0):
 
 def main():
     Ts, B = 0.05, 1024
-    for N in (8, 20, 30, 40, 41, 60, 100):
+    for N in [int(v) for v in (sys.argv[1].split(",") if len(sys.argv) > 1 else "8,20,24,30,32,40,41,60,64,65,100,128".split(","))]:
         x0, up, pr, vr = instances(B, N, Ts)
         d = [torch.as_tensor(a, device="cuda") for a in (x0, up, pr, vr)]
         cfg = TB.config_struct(N=N, Ts=Ts)

@@ -28,8 +28,17 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
     d = dbg.cpu().numpy()
     names = ["inputs", "condense", "scale", "solve", "outputs"]
     idx = [0, 1, 4, 5, 6, 7]
-    ph = np.diff(d[:, idx], axis=1)
-    print(f"kernel {e0.elapsed_time(e1):.3f} ms  B={B} N={N} kind={kind} polish_mode={polish_mode}")
+    ph_all = np.diff(d[:, idx], axis=1)
+    # an item that ends before the ADMM (solver error on non-finite data, infeasible up front) writes no solve stamps:
+    # its slots hold an earlier item's values (non-monotone phases, maxima of 1e13 cycles) -- such items are counted
+    # and left out of every statistic below, as are items with 0 ADMM iterations
+    ok = (ph_all >= 0).all(axis=1) & (ph_all < 5e8).all(axis=1) & (d[:, 9] > 0) & (d[:, 7] > d[:, 0])
+    n_bad = int((~ok).sum())
+    d = d[ok]
+    B = d.shape[0]
+    ph = ph_all[ok]
+    print(f"kernel {e0.elapsed_time(e1):.3f} ms  B={B + n_bad} N={N} kind={kind} polish_mode={polish_mode}"
+          f"  ({n_bad} items without an ADMM solve left out: solver error / infeasible up front)")
     print("phase       median      p90       max   (cycles)")
     for i, nm in enumerate(names):
         print(f"{nm:10s} {np.median(ph[:, i]):9.0f} {np.percentile(ph[:, i], 90):9.0f} {ph[:, i].max():9.0f}")
@@ -38,7 +47,6 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
         st0, en = d[:, 22].astype(float), d[:, 23].astype(float)
         t0 = st0.min()
         span = (en.max() - t0) / 100.0
-        busy = (en - st0[np.argsort(np.argsort(np.arange(B)))] ) if False else None
         print("fused launch span %.1f us; workgroup starts: median %.1f p90 %.1f max %.1f us; instance ends: median %.1f"
               " p90 %.1f max %.1f us" % (span, np.median(st0 - t0) / 100, np.percentile(st0 - t0, 90) / 100,
                                          (st0.max() - t0) / 100, np.median(en - t0) / 100,
