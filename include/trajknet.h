@@ -103,6 +103,12 @@ int traj_knet_front_f32(const traj_vehicle_params* p, const traj_knet_limits* li
                         float* x2, void* stream);
 size_t traj_knet_fc2_workspace_bytes(const traj_knet_net* net, int B);
 int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* ws, size_t ws_bytes, void* stream);
+/* How traj_knet_fc2_f32 forms its products (process-wide; returns the previous mode, -1 for a bad mode):
+ *   1 (default): every f32 operand as three bf16 terms (x = h + m + l exactly) on the bf16 matrix cores, six of
+ *                the nine term products (the dropped ones are below 2^-23 |a b|), f32 accumulation;
+ *   0:           the f32 matrix cores (each product exact, f32 accumulation).
+ * Both are float32-accurate sums in a summation order of their own, like any GEMM against the reference's. */
+int traj_knet_set_fc2_mode(int mode);
 int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, const float* ws,
                        const float* m1x_prior, const float* dy, float* h_sigma, float* x_post, float* out,
                        int out_stride_b, int out_stride_c, float* KG_out, void* stream);

@@ -9,6 +9,8 @@
 // single-precision ones (last-ulp differences to the CPU reference).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "../../include/trajknet.h"
 
 namespace {
@@ -650,6 +652,185 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
 }
 
+// FC2 on the bf16 matrix cores with every f32 operand carried as three bf16 terms (the default FC2;
+// traj_knet_set_fc2_mode(0) selects knet_fc2_kernel above).  x = h + m + l exactly: h = bf16(x), m = bf16(x - h),
+// l = bf16(x - h - m), each residual exact in f32 (24 significand bits = 3 x 8).  A product a b is formed from the
+// six bf16 products h_a h_b, h_a m_b, m_a h_b, h_a l_b, l_a h_b, m_a m_b -- each exact in the f32 accumulator --
+// and the three dropped ones (m_a l_b, l_a m_b, l_a l_b) are below 2^-23 |a b|, the size of one f32 rounding
+// of the product.  So the sums carry f32 accuracy (f32 accumulation, different summation order), at six
+// v_mfma_f32_16x16x32_bf16 (16 cycles, 16,384 FLOP each) per 16 x 16 x 32 block where the f32 form needs eight
+// v_mfma_f32_16x16x4_f32 (32 cycles, 2,048 FLOP each): 96 against 256 matrix-core cycles.
+// Same tiling as knet_fc2_kernel (64 sequences x 64 NT hidden units per workgroup, the x2 tile in LDS, wave w's
+// transposed hidden tile in registers as the second product's B operand), K steps of 32:
+//   A = W2a rows: lane (r, g) of h-tile ht, K step c holds W2a[h0 + 16 ht + r][32 c + 8 g .. + 7] (two float4
+//       loads, one K step ahead), split in registers;
+//   B = x2 from the LDS tile: lane (r, g) holds x2[b0 + 16 bt + r][32 c + 8 g .. + 7], split in registers;
+//   second product, K step s over the tile pair (2s, 2s + 1): B element e of lane (r, g) = hidT[16 (2s + e / 4)
+//       + 4 g + e % 4][16 bt + r] = register e % 4 of accumulator (2s + e / 4, bt), so A element e = W2b[j][that
+//       same h] (two float4 runs of W2b's row); an odd NT's last step has a zero upper half.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const __bf16 vh = (__bf16)v[e];
+        const float r1 = __fsub_rn(v[e], (float)vh);
+        const __bf16 vm = (__bf16)r1;
+        h[e] = vh;
+        m[e] = vm;
+        l[e] = (__bf16)__fsub_rn(r1, (float)vm);
+    }
+}
+
+__device__ __forceinline__ void split3(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    split3(v, h, m, l);
+}
+
+// acc += a b over one K step of 32, the six kept products, smallest first
+__device__ __forceinline__ f32x4 mfma6(const bf16x8& ah, const bf16x8& am, const bf16x8& al, const bf16x8& bh,
+                                       const bf16x8& bm, const bf16x8& bl, f32x4 acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bm, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bm, acc, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
+
+template <int NT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2x_kernel(
+    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const float* __restrict__ b2a,
+    const float* __restrict__ W2b, int nout, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the wave partials
+    constexpr int HS = 64 * NT;
+    const int nslab = dH / HS, nbb = (B + F2_BT - 1) / F2_BT;
+    int slab, bblk;
+    const int i = blockIdx.x;
+    if ((nslab & 7) == 0) {   // the b-blocks of a slab on one XCD (its W2a slab stays in that L2)
+        const int xcd = i & 7, local = i >> 3;
+        slab = (local / nbb) * 8 + xcd;
+        bblk = local % nbb;
+    } else {
+        slab = i / nbb;
+        bblk = i % nbb;
+    }
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
+    const int b0 = bblk * F2_BT, hw0 = slab * HS + 16 * NT * w;
+    constexpr int K = 2 * KH;
+#pragma unroll
+    for (int it = 0; it < F2_BT * (K / 4) / 256; ++it) {
+        const int q = t + 256 * it, row = q / (K / 4), c4 = q - row * (K / 4);
+        const int bsrc = min(b0 + row, B - 1);   // rows past B: duplicates, never stored
+        *reinterpret_cast<float4*>(s_t + row * F2_LD + 4 * c4) = reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
+    }
+    const float* pa = W2a + (size_t)(hw0 + r) * K + 8 * g;   // h-tile ht: + 16 ht K; K step c: + 32 c
+    constexpr int NC = K / 32;
+    float4 an[NT][2];
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht) {
+        an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K);
+        an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 4);
+    }
+    __syncthreads();
+    f32x4 acc[NT][4];
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) acc[ht][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float* xr = s_t + r * F2_LD + 8 * g;
+    for (int c = 0; c < NC; ++c) {
+        bf16x8 ah[NT], am[NT], al[NT];
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
+        if (c + 1 < NC) {
+#pragma unroll
+            for (int ht = 0; ht < NT; ++ht) {
+                an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * (c + 1));
+                an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * (c + 1) + 4);
+            }
+        }
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+            const float4* xp = reinterpret_cast<const float4*>(xr + 16 * bt * F2_LD + 32 * c);
+            bf16x8 bh, bm, bl;
+            split3(xp[0], xp[1], bh, bm, bl);
+#pragma unroll
+            for (int ht = 0; ht < NT; ++ht) acc[ht][bt] = mfma6(ah[ht], am[ht], al[ht], bh, bm, bl, acc[ht][bt]);
+        }
+    }
+    // relu(hidT + b2a) in place (register q of lane (g, r) in tile (ht, bt): unit hw0 + 16 ht + 4 g + q, sequence
+    // b0 + 16 bt + r)
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht) {
+        const float4 bias = *reinterpret_cast<const float4*>(b2a + hw0 + 16 * ht + 4 * g);
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[ht][bt][q] = fmaxf(__fadd_rn(acc[ht][bt][q], f4c(bias, q)), 0.0f);
+    }
+    // outT[j][b] = sum over this wave's units of W2b[j][h] hidT[h][b] (rows j = 16 jt + r; rows >= nout: zero)
+    const float m0 = r < nout ? 1.0f : 0.0f, m1 = 16 + r < nout ? 1.0f : 0.0f;
+    const float* pb[2] = {W2b + (size_t)min(r, nout - 1) * dH + hw0 + 4 * g,
+                          W2b + (size_t)min(16 + r, nout - 1) * dH + hw0 + 4 * g};
+    const float mk[2] = {m0, m1};
+    f32x4 o[2][4];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) o[jt][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < (NT + 1) / 2; ++s) {
+        constexpr float z = 0.0f;
+        const bool hi2 = 2 * s + 1 < NT;   // the step's upper tile exists
+        bf16x8 wh[2], wm[2], wl[2];
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+            float4 u0 = *reinterpret_cast<const float4*>(pb[jt] + 32 * s);
+            float4 u1 = hi2 ? *reinterpret_cast<const float4*>(pb[jt] + 32 * s + 16) : make_float4(z, z, z, z);
+            const float v[8] = {u0.x * mk[jt], u0.y * mk[jt], u0.z * mk[jt], u0.w * mk[jt],
+                                u1.x * mk[jt], u1.y * mk[jt], u1.z * mk[jt], u1.w * mk[jt]};
+            split3(v, wh[jt], wm[jt], wl[jt]);
+        }
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = acc[2 * s][bt][e];
+                v[4 + e] = hi2 ? acc[hi2 ? 2 * s + 1 : 2 * s][bt][e] : 0.0f;
+            }
+            bf16x8 bh, bm, bl;
+            split3(v, bh, bm, bl);
+#pragma unroll
+            for (int jt = 0; jt < 2; ++jt) o[jt][bt] = mfma6(wh[jt], wm[jt], wl[jt], bh, bm, bl, o[jt][bt]);
+        }
+    }
+    __syncthreads();   // every wave is done with the x2 tile
+    float* red = s_t + w * 32 * F2_RS;
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) red[(16 * jt + 4 * g + q) * F2_RS + 16 * bt + r] = o[jt][bt][q];
+    __syncthreads();
+    {   // thread t: sequence t >> 2, outputs 8 (t & 3) .. + 7; waves added in order
+        const int bb = t >> 2, j0 = 8 * (t & 3);
+        float v[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+            const float* p0 = s_t + (j0 + jj) * F2_RS + bb;
+            v[jj] = __fadd_rn(__fadd_rn(__fadd_rn(p0[0], p0[32 * F2_RS]), p0[64 * F2_RS]), p0[96 * F2_RS]);
+        }
+        if (b0 + bb < B) {
+            float4* dst = reinterpret_cast<float4*>(part + ((size_t)slab * B + b0 + bb) * 32 + j0);
+            dst[0] = make_float4(v[0], v[1], v[2], v[3]);
+            dst[1] = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    }
+}
+
 __device__ __forceinline__ void back_body(KNet net, int B, const float* __restrict__ x2,
                                                        const float* __restrict__ part, int nslab,
                                                        const float* __restrict__ prior, const float* __restrict__ dy,
@@ -1012,6 +1193,9 @@ inline int nblk(long long n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
 
+// traj_knet_set_fc2_mode: 1 = knet_fc2x_kernel (three-term bf16 operands, the default), 0 = knet_fc2_kernel (f32)
+static std::atomic<int> g_fc2_mode{1};
+
 extern "C" {
 
 int traj_knet_prior_f32(const traj_vehicle_params* p, const traj_knet_limits* lim, float Ts, int B,
@@ -1150,13 +1334,17 @@ int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* w
         ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2a_b & 15) || ((uintptr_t)net->fc2b_w & 15))
         return TRAJ_E_ARG;
     const int hs = fc2_slab(net->d_fc2h), nslab = net->d_fc2h / hs, nbb = nblk(B, F2_BT);
-    if (hs == 320)
-        hipLaunchKernelGGL(knet_fc2_kernel<5>, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h,
-                           x2, net->fc2a_w, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
-    else
-        hipLaunchKernelGGL(knet_fc2_kernel<4>, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h,
-                           x2, net->fc2a_w, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
+    const bool split = g_fc2_mode.load(std::memory_order_relaxed) != 0;
+    auto kern = hs == 320 ? (split ? knet_fc2x_kernel<5> : knet_fc2_kernel<5>)
+                          : (split ? knet_fc2x_kernel<4> : knet_fc2_kernel<4>);
+    hipLaunchKernelGGL(kern, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w,
+                       net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+int traj_knet_set_fc2_mode(int mode) {
+    if (mode != 0 && mode != 1) return -1;
+    return g_fc2_mode.exchange(mode);
 }
 
 int traj_knet_back_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, const float* ws,
