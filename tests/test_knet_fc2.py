@@ -25,17 +25,25 @@ def _model(dev, out_mult, seed=3):
     return K, model
 
 
-def _fc2(K, model, x2, mode):
+def _fc2(K, model, x2, mode, packed=False):
     from trajectory_generation_amd import _lib
     L = _lib.lib()
     net = K.net_struct(model)
     B = x2.shape[0]
     ws = torch.full((L.traj_knet_fc2_workspace_bytes(C.byref(net), B) // 4,), float("nan"), device=x2.device)
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     prev = L.traj_knet_set_fc2_mode(mode)
     try:
-        _lib.check(L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()),
-                                       ws.numel() * 4, C.c_void_p(torch.cuda.current_stream().cuda_stream)),
-                   "traj_knet_fc2_f32")
+        if packed:
+            nb = L.traj_knet_packed_bytes(C.byref(net))
+            pk = torch.empty(nb // 4, dtype=torch.float32, device=x2.device)
+            _lib.check(L.traj_knet_pack_f32(C.byref(net), C.c_void_p(pk.data_ptr()), nb, st), "traj_knet_pack_f32")
+            _lib.check(L.traj_knet_fc2_packed_f32(C.byref(net), C.c_void_p(pk.data_ptr()), B, C.c_void_p(x2.data_ptr()),
+                                                  C.c_void_p(ws.data_ptr()), ws.numel() * 4, st),
+                       "traj_knet_fc2_packed_f32")
+        else:
+            _lib.check(L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()),
+                                           ws.numel() * 4, st), "traj_knet_fc2_f32")
     finally:
         L.traj_knet_set_fc2_mode(prev)
     torch.cuda.synchronize()
@@ -63,19 +71,27 @@ def test_fc2_modes_vs_float64(gpu, out_mult, B):
     ref = hid @ Wb.T + bb
     scale = np.abs(bb) + np.maximum(np.abs(xd) @ np.abs(Wa).T + np.abs(ba), 0.0) @ np.abs(Wb).T
     errs = {}
-    for mode in (0, 1):
-        out = _fc2(K, model, x2, mode)
+    outs = {}
+    for mode, packed in ((0, False), (1, False), (1, True), (0, True), (2, True), (3, True)):
+        out = _fc2(K, model, x2, mode, packed)
         assert np.isfinite(out).all()
         rel = np.abs(out - ref) / scale
-        assert rel.max() <= 1e-6, (mode, rel.max())
-        errs[mode] = rel.max()
-    assert errs[1] <= 2.0 * errs[0] + 1e-7, errs
+        assert rel.max() <= 1e-6, (mode, packed, rel.max())
+        errs[mode, packed] = rel.max()
+        outs[mode, packed] = out
+    assert errs[1, False] <= 2.0 * errs[0, False] + 1e-7, errs
+    # the weight split once at pack time or in every workgroup: the same terms, the same sums
+    np.testing.assert_array_equal(outs[1, True], outs[1, False])
+    np.testing.assert_array_equal(outs[0, True], outs[0, False])
+    # the x2 tile split once per workgroup into LDS planes (mode 2): the same terms in the same order
+    np.testing.assert_array_equal(outs[2, True], outs[1, True])
+    np.testing.assert_array_equal(outs[3, True], outs[1, True])
 
 
 def test_fc2_mode_switch(gpu):
     from trajectory_generation_amd import _lib
     L = _lib.lib()
-    assert L.traj_knet_set_fc2_mode(5) == -1
+    assert L.traj_knet_set_fc2_mode(4) == -1 and L.traj_knet_set_fc2_mode(-1) == -1
     prev = L.traj_knet_set_fc2_mode(0)
-    assert prev in (0, 1)
+    assert prev in (0, 1, 2, 3)
     assert L.traj_knet_set_fc2_mode(prev) == 0

@@ -34,9 +34,19 @@ def main(B=1024, T=200, reps=5):
     x2 = torch.relu(torch.randn(B, 256, device=dev))
     ws = torch.empty(L.traj_knet_fc2_workspace_bytes(C.byref(net), B) // 4, device=dev)
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    nb = L.traj_knet_packed_bytes(C.byref(net))
+    pk = torch.empty(nb // 4, device=dev)
+    L.traj_knet_pack_f32(C.byref(net), C.c_void_p(pk.data_ptr()), nb, st)
+
+    def fc2(packed):
+        if packed:
+            return L.traj_knet_fc2_packed_f32(C.byref(net), C.c_void_p(pk.data_ptr()), B, C.c_void_p(x2.data_ptr()),
+                                              C.c_void_p(ws.data_ptr()), ws.numel() * 4, st)
+        return L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()),
+                                   ws.numel() * 4, st)
     res = {}
     outs = {}
-    for mode in (0, 1, 0, 1):
+    for mode in (0, 1, 2, 3, 0, 1, 2, 3):
         L.traj_knet_set_fc2_mode(mode)
         run = K.KNetSequenceRunner(model, B)
         out = run.run(y, u, m1x0, fused=True)   # capture + warm
@@ -48,22 +58,23 @@ def main(B=1024, T=200, reps=5):
             torch.cuda.synchronize()
             best = min(best, time.perf_counter() - t0)
         outs[mode] = out.cpu().numpy()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for _ in range(5):
-            L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()), ws.numel() * 4, st)
-        e0.record()
-        for _ in range(50):
-            L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()), ws.numel() * 4, st)
-        e1.record()
-        torch.cuda.synchronize()
-        fc2_us = e0.elapsed_time(e1) * 1e3 / 50
         key = f"mode{mode}"
-        r = res.setdefault(key, {"seq_per_s": [], "step_us": [], "fc2_us": []})
+        r = res.setdefault(key, {"seq_per_s": [], "step_us": [], "fc2_us": [], "fc2_packed_us": []})
         r["seq_per_s"].append(round(B / best, 1))
         r["step_us"].append(round(best / T * 1e6, 2))
-        r["fc2_us"].append(round(fc2_us, 2))
+        for packed in (False, True):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(5):
+                fc2(packed)
+            e0.record()
+            for _ in range(50):
+                fc2(packed)
+            e1.record()
+            torch.cuda.synchronize()
+            r["fc2_packed_us" if packed else "fc2_us"].append(round(e0.elapsed_time(e1) * 1e3 / 50, 2))
     L.traj_knet_set_fc2_mode(1)
     res["max_abs_diff_posteriors"] = float(np.abs(outs[0] - outs[1]).max())
+    res["modes_1_2_3_identical"] = bool(np.array_equal(outs[1], outs[2]) and np.array_equal(outs[1], outs[3]))
     res["max_abs_posterior"] = float(np.abs(outs[0]).max())
     flop = B * 2 * (256 * 10240 + 10240 * 30)
     res["fc2_flop"] = flop

@@ -220,9 +220,11 @@ struct KNet {
 __host__ __device__ inline int k4_(int K) { return ((K + 63) / 64) * 16; }
 
 // Packed-buffer offsets (in floats) of the eleven matrices, in the order of traj_knet_net.
+// off[11]: FC2.0's weight as three bf16 planes (hi, mid, lo; row-major [d_fc2h][2H] each) for knet_fc2x_kernel; off[12]:
+// the end.
 struct PackPlan {
     int N[11], K[11];
-    size_t off[12];
+    size_t off[13];
 };
 static PackPlan pack_plan(const traj_knet_net* w) {
     PackPlan pl{};
@@ -235,6 +237,7 @@ static PackPlan pack_plan(const traj_knet_net* w) {
         pl.K[i] = K[i];
         pl.off[i + 1] = pl.off[i] + (size_t)4 * k4_(K[i]) * N[i];
     }
+    pl.off[12] = pl.off[11] + (size_t)3 * w->d_fc2h * (2 * H) / 2;   // bf16 planes, in floats
     return pl;
 }
 
@@ -670,16 +673,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 //       same h] (two float4 runs of W2b's row); an odd NT's last step has a zero upper half.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+// (the subtractions may pair into v_pk_add_f32: measured 35.0 us for the FC2 launch against 37.4 us with single
+// v_sub_f32 forced by inline asm)
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r1 = __fsub_rn(x, (float)h);
+    m = (__bf16)r1;
+    l = (__bf16)__fsub_rn(r1, (float)m);
+}
+
 __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-        const __bf16 vh = (__bf16)v[e];
-        const float r1 = __fsub_rn(v[e], (float)vh);
-        const __bf16 vm = (__bf16)r1;
+        __bf16 vh, vm, vl;
+        split3(v[e], vh, vm, vl);
         h[e] = vh;
         m[e] = vm;
-        l[e] = (__bf16)__fsub_rn(r1, (float)vm);
+        l[e] = vl;
     }
+}
+
+// FC2.0's weight [n = d_fc2h x 2H] into the three planes of the packed buffer (knet_fc2x_kernel<NT, true>)
+__global__ void knet_split_kernel(const float* __restrict__ W, long long n, __bf16* __restrict__ Pl) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    __bf16 h, m, l;
+    split3(W[i], h, m, l);
+    Pl[i] = h;
+    Pl[n + i] = m;
+    Pl[2 * n + i] = l;
 }
 
 __device__ __forceinline__ void split3(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
@@ -698,67 +720,14 @@ __device__ __forceinline__ f32x4 mfma6(const bf16x8& ah, const bf16x8& am, const
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
 }
 
+// The three-term kernels' second half: relu(hidT + b2a) in the accumulators, the second product on the bf16 matrix
+// cores (B = the accumulators, A = W2b split in registers), the four waves' partials added in wave order through LDS
+// (s_red: 4 x 32 x F2_RS floats, free once every wave is past its reads of the tile), part[slab][b][0:32] written.
 template <int NT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2x_kernel(
-    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const float* __restrict__ b2a,
-    const float* __restrict__ W2b, int nout, float* __restrict__ part) {
-    __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the wave partials
-    constexpr int HS = 64 * NT;
-    const int nslab = dH / HS, nbb = (B + F2_BT - 1) / F2_BT;
-    int slab, bblk;
-    const int i = blockIdx.x;
-    if ((nslab & 7) == 0) {   // the b-blocks of a slab on one XCD (its W2a slab stays in that L2)
-        const int xcd = i & 7, local = i >> 3;
-        slab = (local / nbb) * 8 + xcd;
-        bblk = local % nbb;
-    } else {
-        slab = i / nbb;
-        bblk = i % nbb;
-    }
+__device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][4], const float* __restrict__ b2a,
+                                              const float* __restrict__ W2b, int dH, int nout, int hw0, int B, int b0,
+                                              int slab, float* s_red, float* __restrict__ part) {
     const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
-    const int b0 = bblk * F2_BT, hw0 = slab * HS + 16 * NT * w;
-    constexpr int K = 2 * KH;
-#pragma unroll
-    for (int it = 0; it < F2_BT * (K / 4) / 256; ++it) {
-        const int q = t + 256 * it, row = q / (K / 4), c4 = q - row * (K / 4);
-        const int bsrc = min(b0 + row, B - 1);   // rows past B: duplicates, never stored
-        *reinterpret_cast<float4*>(s_t + row * F2_LD + 4 * c4) = reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
-    }
-    const float* pa = W2a + (size_t)(hw0 + r) * K + 8 * g;   // h-tile ht: + 16 ht K; K step c: + 32 c
-    constexpr int NC = K / 32;
-    float4 an[NT][2];
-#pragma unroll
-    for (int ht = 0; ht < NT; ++ht) {
-        an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K);
-        an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 4);
-    }
-    __syncthreads();
-    f32x4 acc[NT][4];
-#pragma unroll
-    for (int ht = 0; ht < NT; ++ht)
-#pragma unroll
-        for (int bt = 0; bt < 4; ++bt) acc[ht][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    const float* xr = s_t + r * F2_LD + 8 * g;
-    for (int c = 0; c < NC; ++c) {
-        bf16x8 ah[NT], am[NT], al[NT];
-#pragma unroll
-        for (int ht = 0; ht < NT; ++ht) split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
-        if (c + 1 < NC) {
-#pragma unroll
-            for (int ht = 0; ht < NT; ++ht) {
-                an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * (c + 1));
-                an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * (c + 1) + 4);
-            }
-        }
-#pragma unroll
-        for (int bt = 0; bt < 4; ++bt) {
-            const float4* xp = reinterpret_cast<const float4*>(xr + 16 * bt * F2_LD + 32 * c);
-            bf16x8 bh, bm, bl;
-            split3(xp[0], xp[1], bh, bm, bl);
-#pragma unroll
-            for (int ht = 0; ht < NT; ++ht) acc[ht][bt] = mfma6(ah[ht], am[ht], al[ht], bh, bm, bl, acc[ht][bt]);
-        }
-    }
     // relu(hidT + b2a) in place (register q of lane (g, r) in tile (ht, bt): unit hw0 + 16 ht + 4 g + q, sequence
     // b0 + 16 bt + r)
 #pragma unroll
@@ -806,8 +775,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             for (int jt = 0; jt < 2; ++jt) o[jt][bt] = mfma6(wh[jt], wm[jt], wl[jt], bh, bm, bl, o[jt][bt]);
         }
     }
-    __syncthreads();   // every wave is done with the x2 tile
-    float* red = s_t + w * 32 * F2_RS;
+    __syncthreads();   // every wave is done with the tile in LDS
+    float* red = s_red + w * 32 * F2_RS;
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
@@ -820,7 +789,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         float v[8];
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-            const float* p0 = s_t + (j0 + jj) * F2_RS + bb;
+            const float* p0 = s_red + (j0 + jj) * F2_RS + bb;
             v[jj] = __fadd_rn(__fadd_rn(__fadd_rn(p0[0], p0[32 * F2_RS]), p0[64 * F2_RS]), p0[96 * F2_RS]);
         }
         if (b0 + bb < B) {
@@ -829,6 +798,201 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
             dst[1] = make_float4(v[4], v[5], v[6], v[7]);
         }
     }
+}
+
+// PRE: A from the packed buffer's three planes of W2a (split once at pack time; one 16-byte load per plane), else
+// W2a split in registers as it streams in.
+template <int NT, bool PRE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2x_kernel(
+    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const __bf16* __restrict__ Wp,
+    const float* __restrict__ b2a, const float* __restrict__ W2b, int nout, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the wave partials
+    constexpr int HS = 64 * NT;
+    const int nslab = dH / HS, nbb = (B + F2_BT - 1) / F2_BT;
+    int slab, bblk;
+    const int i = blockIdx.x;
+    if ((nslab & 7) == 0) {   // the b-blocks of a slab on one XCD (its W2a slab stays in that L2)
+        const int xcd = i & 7, local = i >> 3;
+        slab = (local / nbb) * 8 + xcd;
+        bblk = local % nbb;
+    } else {
+        slab = i / nbb;
+        bblk = i % nbb;
+    }
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
+    const int b0 = bblk * F2_BT, hw0 = slab * HS + 16 * NT * w;
+    constexpr int K = 2 * KH;
+#pragma unroll
+    for (int it = 0; it < F2_BT * (K / 4) / 256; ++it) {
+        const int q = t + 256 * it, row = q / (K / 4), c4 = q - row * (K / 4);
+        const int bsrc = min(b0 + row, B - 1);   // rows past B: duplicates, never stored
+        *reinterpret_cast<float4*>(s_t + row * F2_LD + 4 * c4) = reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
+    }
+    const float* pa = W2a + (size_t)(hw0 + r) * K + 8 * g;   // h-tile ht: + 16 ht K; K step c: + 32 c
+    const size_t pln = (size_t)dH * K;                        // PRE: plane stride
+    const __bf16* pp = Wp + (size_t)(hw0 + r) * K + 8 * g;
+    constexpr int NC = K / 32;
+    float4 an[PRE ? 1 : NT][2];
+    bf16x8 apn[PRE ? NT : 1][3];
+    auto load_a = [&](int c) {
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) {
+            if constexpr (PRE) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    apn[ht][q] = *reinterpret_cast<const bf16x8*>(pp + q * pln + (size_t)16 * ht * K + 32 * c);
+            } else {
+                an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c);
+                an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c + 4);
+            }
+        }
+    };
+    load_a(0);
+    __syncthreads();
+    f32x4 acc[NT][4];
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) acc[ht][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const float* xr = s_t + r * F2_LD + 8 * g;
+    for (int c = 0; c < NC; ++c) {
+        bf16x8 ah[NT], am[NT], al[NT];
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) {
+            if constexpr (PRE) {
+                ah[ht] = apn[ht][0];
+                am[ht] = apn[ht][1];
+                al[ht] = apn[ht][2];
+            } else {
+                split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
+            }
+        }
+        if (c + 1 < NC) load_a(c + 1);
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+            const float4* xp = reinterpret_cast<const float4*>(xr + 16 * bt * F2_LD + 32 * c);
+            bf16x8 bh, bm, bl;
+            split3(xp[0], xp[1], bh, bm, bl);
+#pragma unroll
+            for (int ht = 0; ht < NT; ++ht) acc[ht][bt] = mfma6(ah[ht], am[ht], al[ht], bh, bm, bl, acc[ht][bt]);
+        }
+    }
+    fc2x_epilogue<NT>(acc, b2a, W2b, dH, nout, hw0, B, b0, slab, s_t, part);
+}
+
+// The three-term FC2 with the x2 tile split ONCE per workgroup (knet_fc2x_kernel has every wave split all 64 sequences'
+// values at every K step): the tile's three bf16 planes in LDS, one K half at a time (52 KB, so two workgroups still
+// share a CU), W2a split in registers as in knet_fc2x_kernel.  Same terms, same summation order, bit for bit.
+constexpr int F2_HK = KH;            // K columns per half
+constexpr int F2_BLD = F2_HK + 8;    // bf16 per LDS plane row (272 B: rows 4 banks apart)
+
+template <int NT, bool PRE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2y_kernel(
+    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const __bf16* __restrict__ Wp,
+    const float* __restrict__ b2a, const float* __restrict__ W2b, int nout, float* __restrict__ part) {
+    constexpr int PL = F2_BT * F2_BLD;
+    __shared__ __attribute__((aligned(16))) __bf16 s_b[3 * PL];   // one K half of the tile: hi, mid, lo planes
+    static_assert(4 * 32 * F2_RS * sizeof(float) <= sizeof(s_b), "partials fit the planes");
+    constexpr int HS = 64 * NT;
+    const int nslab = dH / HS, nbb = (B + F2_BT - 1) / F2_BT;
+    int slab, bblk;
+    const int i = blockIdx.x;
+    if ((nslab & 7) == 0) {
+        const int xcd = i & 7, local = i >> 3;
+        slab = (local / nbb) * 8 + xcd;
+        bblk = local % nbb;
+    } else {
+        slab = i / nbb;
+        bblk = i % nbb;
+    }
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
+    const int b0 = bblk * F2_BT, hw0 = slab * HS + 16 * NT * w;
+    constexpr int K = 2 * KH, NC = K / 32;
+#ifndef TRAJ_FC2_EXP
+#define TRAJ_FC2_EXP 0   // timing experiments only (wrong results): 1 = every slab reads slab 0's W2a rows, 2 = K step
+#endif                   // 0's A for every K step
+    const float* pa = W2a + (size_t)((TRAJ_FC2_EXP == 1 ? 16 * NT * w : hw0) + r) * K + 8 * g;
+    const size_t pln = (size_t)dH * K;
+    const __bf16* pp = Wp + (size_t)(hw0 + r) * K + 8 * g;
+    float4 an[PRE ? 1 : NT][2];
+    bf16x8 apn[PRE ? NT : 1][3];
+    auto load_a = [&](int c) {
+        if (TRAJ_FC2_EXP == 2 && c > 0) return;
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) {
+            if constexpr (PRE) {
+#pragma unroll
+                for (int q = 0; q < 3; ++q)
+                    apn[ht][q] = *reinterpret_cast<const bf16x8*>(pp + q * pln + (size_t)16 * ht * K + 32 * c);
+            } else {
+                an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c);
+                an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c + 4);
+            }
+        }
+    };
+    // half hf of the tile, split: thread t takes float4 q = t + 256 it (row q / 32, columns hf 128 + 4 (q % 32) .. + 3)
+    auto stage = [&](int hf) {
+#pragma unroll 4
+        for (int it = 0; it < F2_BT * (F2_HK / 4) / 256; ++it) {
+            const int q = t + 256 * it, row = q / (F2_HK / 4), c4 = q - row * (F2_HK / 4);
+            const int bsrc = min(b0 + row, B - 1);   // rows past B: duplicates, never stored
+            const float4 v = reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K + hf * F2_HK)[c4];
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            bf16x4 h, m, lo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                __bf16 a0, a1, a2;
+                split3(vv[e], a0, a1, a2);
+                h[e] = a0;
+                m[e] = a1;
+                lo[e] = a2;
+            }
+            const int o = row * F2_BLD + 4 * c4;
+            *reinterpret_cast<bf16x4*>(s_b + o) = h;
+            *reinterpret_cast<bf16x4*>(s_b + PL + o) = m;
+            *reinterpret_cast<bf16x4*>(s_b + 2 * PL + o) = lo;
+        }
+    };
+    load_a(0);
+    stage(0);
+    __syncthreads();
+    f32x4 acc[NT][4];
+#pragma unroll
+    for (int ht = 0; ht < NT; ++ht)
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) acc[ht][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    const __bf16* xr = s_b + r * F2_BLD + 8 * g;
+    for (int c = 0; c < NC; ++c) {
+        if (c == NC / 2) {   // second K half
+            __syncthreads();
+            stage(1);
+            __syncthreads();
+        }
+        bf16x8 ah[NT], am[NT], al[NT];
+#pragma unroll
+        for (int ht = 0; ht < NT; ++ht) {
+            if constexpr (PRE) {
+                ah[ht] = apn[ht][0];
+                am[ht] = apn[ht][1];
+                al[ht] = apn[ht][2];
+            } else {
+                split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
+            }
+        }
+        if (c + 1 < NC) load_a(c + 1);
+        const int cc = c & (NC / 2 - 1);
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {
+            const __bf16* bp = xr + 16 * bt * F2_BLD + 32 * cc;
+            const bf16x8 bh = *reinterpret_cast<const bf16x8*>(bp);
+            const bf16x8 bm = *reinterpret_cast<const bf16x8*>(bp + PL);
+            const bf16x8 bl = *reinterpret_cast<const bf16x8*>(bp + 2 * PL);
+#pragma unroll
+            for (int ht = 0; ht < NT; ++ht) acc[ht][bt] = mfma6(ah[ht], am[ht], al[ht], bh, bm, bl, acc[ht][bt]);
+        }
+    }
+    fc2x_epilogue<NT>(acc, b2a, W2b, dH, nout, hw0, B, b0, slab, reinterpret_cast<float*>(s_b), part);
 }
 
 __device__ __forceinline__ void back_body(KNet net, int B, const float* __restrict__ x2,
@@ -1193,8 +1357,35 @@ inline int nblk(long long n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
 
-// traj_knet_set_fc2_mode: 1 = knet_fc2x_kernel (three-term bf16 operands, the default), 0 = knet_fc2_kernel (f32)
-static std::atomic<int> g_fc2_mode{1};
+// traj_knet_set_fc2_mode: 2 = knet_fc2y_kernel (three-term bf16 operands, the tile split once per workgroup; the
+// default), 1 = knet_fc2x_kernel (the same terms, every wave splitting the tile), 3 = knet_fc2y_kernel with W2a's planes
+// from the packed buffer, 0 = knet_fc2_kernel (f32).  Modes 1-3 give identical results.
+static std::atomic<int> g_fc2_mode{2};
+
+// FC2 launch: packed != NULL takes W2a's bf16 planes from the packed buffer (traj_knet_fc2_packed_f32)
+static int fc2_launch(const traj_knet_net* net, const float* packed, int B, const float* x2, float* ws, void* stream) {
+    const int hs = fc2_slab(net->d_fc2h), nslab = net->d_fc2h / hs, nbb = nblk(B, F2_BT);
+    const int mode = g_fc2_mode.load(std::memory_order_relaxed);
+    const bool split = mode != 0;
+    const __bf16* wp = packed ? reinterpret_cast<const __bf16*>(packed + pack_plan(net).off[11]) : nullptr;
+    if (mode >= 2) {
+        auto ky = hs == 320 ? (mode == 3 && wp ? knet_fc2y_kernel<5, true> : knet_fc2y_kernel<5, false>)
+                            : (mode == 3 && wp ? knet_fc2y_kernel<4, true> : knet_fc2y_kernel<4, false>);
+        hipLaunchKernelGGL(ky, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w,
+                           wp, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
+        return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+    }
+    auto kern = hs == 320 ? (wp ? knet_fc2x_kernel<5, true> : knet_fc2x_kernel<5, false>)
+                          : (wp ? knet_fc2x_kernel<4, true> : knet_fc2x_kernel<4, false>);
+    if (split)
+        hipLaunchKernelGGL(kern, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2,
+                           net->fc2a_w, wp, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
+    else
+        hipLaunchKernelGGL(hs == 320 ? knet_fc2_kernel<5> : knet_fc2_kernel<4>, dim3(nslab * nbb), dim3(256), 0,
+                           (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w, net->fc2a_b, net->fc2b_w,
+                           net->n * net->m, ws);
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
 
 extern "C" {
 
@@ -1281,14 +1472,14 @@ static KNet knet_args(const traj_knet_net* w, const float* packed) {
 
 size_t traj_knet_packed_bytes(const traj_knet_net* net) {
     if (!knet_ok(net)) return 0;
-    return pack_plan(net).off[11] * sizeof(float);
+    return pack_plan(net).off[12] * sizeof(float);
 }
 
 int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, void* stream) {
     if (!net || !packed) return TRAJ_E_ARG;
     if (!knet_ok(net)) return TRAJ_E_UNSUPPORTED;
     const PackPlan pl = pack_plan(net);
-    if (bytes < pl.off[11] * sizeof(float) || ((uintptr_t)packed & 15)) return TRAJ_E_ARG;
+    if (bytes < pl.off[12] * sizeof(float) || ((uintptr_t)packed & 15)) return TRAJ_E_ARG;
     const float* W[11] = {net->fc5_w, net->gru_q_wih, net->gru_q_whh, net->gru_sigma_wih, net->gru_sigma_whh,
                           net->fc1_w, net->fc7_w,     net->gru_s_wih, net->gru_s_whh,     net->fc3_w,
                           net->fc4_w};
@@ -1297,6 +1488,9 @@ int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, vo
         hipLaunchKernelGGL(knet_pack_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, W[i], pl.N[i],
                            pl.K[i], packed + pl.off[i]);
     }
+    const long long n2 = (long long)net->d_fc2h * 2 * net->hidden;
+    hipLaunchKernelGGL(knet_split_kernel, dim3(nblk(n2, 256)), dim3(256), 0, (hipStream_t)stream, net->fc2a_w, n2,
+                       reinterpret_cast<__bf16*>(packed + pl.off[11]));
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
@@ -1334,16 +1528,23 @@ int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* w
         ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2a_b & 15) || ((uintptr_t)net->fc2b_w & 15))
         return TRAJ_E_ARG;
     const int hs = fc2_slab(net->d_fc2h), nslab = net->d_fc2h / hs, nbb = nblk(B, F2_BT);
-    const bool split = g_fc2_mode.load(std::memory_order_relaxed) != 0;
-    auto kern = hs == 320 ? (split ? knet_fc2x_kernel<5> : knet_fc2_kernel<5>)
-                          : (split ? knet_fc2x_kernel<4> : knet_fc2_kernel<4>);
-    hipLaunchKernelGGL(kern, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w,
-                       net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
-    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+    return fc2_launch(net, nullptr, B, x2, ws, stream);
+}
+
+int traj_knet_fc2_packed_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, float* ws,
+                             size_t ws_bytes, void* stream) {
+    if (B < 0) return TRAJ_E_ARG;
+    if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
+    if (B == 0) return TRAJ_OK;
+    if (!packed || ((uintptr_t)packed & 15) || !x2 || !ws || ws_bytes < traj_knet_fc2_workspace_bytes(net, B) ||
+        ((uintptr_t)x2 & 15) || ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2a_b & 15) ||
+        ((uintptr_t)net->fc2b_w & 15))
+        return TRAJ_E_ARG;
+    return fc2_launch(net, packed, B, x2, ws, stream);
 }
 
 int traj_knet_set_fc2_mode(int mode) {
-    if (mode != 0 && mode != 1) return -1;
+    if (mode < 0 || mode > 3) return -1;
     return g_fc2_mode.exchange(mode);
 }
 
