@@ -77,9 +77,8 @@ typedef struct {
 
 /* The fused kernels read the eleven weight matrices from a packed copy made once per set of weights:
  * traj_knet_packed_bytes(net) bytes (0 for unsupported shapes), filled by traj_knet_pack_f32 on
- * `stream` (16-byte aligned buffer; layout P[k4][j][4] = W[j][4 k4 + c], zero past K), followed by FC2.0's
- * weight as three bf16 planes (traj_knet_fc2_packed_f32).  Biases and innov_logit are read through `net` itself,
- * so its pointers must stay valid while the kernels run. */
+ * `stream` (16-byte aligned buffer; layout P[k4][j][4] = W[j][4 k4 + c], zero past K).  Biases and
+ * innov_logit are read through `net` itself, so its pointers must stay valid while the kernels run. */
 size_t traj_knet_packed_bytes(const traj_knet_net* net);
 int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, void* stream);
 
@@ -104,14 +103,10 @@ int traj_knet_front_f32(const traj_vehicle_params* p, const traj_knet_limits* li
                         float* x2, void* stream);
 size_t traj_knet_fc2_workspace_bytes(const traj_knet_net* net, int B);
 int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* ws, size_t ws_bytes, void* stream);
-/* traj_knet_fc2_f32 with the packed buffer of traj_knet_pack_f32 (which holds FC2.0's weight pre-split for the
- * default mode below): the same sums, without re-splitting the weight in every workgroup.  The fused runner's form. */
-int traj_knet_fc2_packed_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, float* ws,
-                             size_t ws_bytes, void* stream);
-/* How traj_knet_fc2_f32 / traj_knet_fc2_packed_f32 form their products (process-wide; returns the previous mode, -1 for a bad mode):
+/* How traj_knet_fc2_f32 forms its products (process-wide; returns the previous mode, -1 for a bad mode):
  *   2 (default): every f32 operand as three bf16 terms (x = h + m + l exactly) on the bf16 matrix cores, six of
  *                the nine term products (the dropped ones are below 2^-23 |a b|), f32 accumulation;
- *   1, 3:        the same terms and sums as 2 (bit-identical), organized differently (kernel-variant experiments);
+ *   1:           the same terms and sums as 2 (bit-identical), every wave splitting the input tile itself;
  *   0:           the f32 matrix cores (each product exact, f32 accumulation).
  * All are float32-accurate sums in a summation order of their own, like any GEMM against the reference's. */
 int traj_knet_set_fc2_mode(int mode);

@@ -1,8 +1,9 @@
 """FC2 of the fused KalmanNet step (traj_knet_fc2_f32, kalman_net.py:88-95 / :186: Linear(2H, dH) -> ReLU ->
-Linear(dH, n m)) in both product modes (traj_knet_set_fc2_mode): the three-term bf16 form (default) and the f32
-matrix-core form, each against a float64 evaluation of the same weights and inputs.  Bar: a float32 GEMM's
-accuracy, |err| <= 1e-6 x (|b| + |W2b| relu(|W2a| |x2| + |b2a|)) elementwise (the f32 rounding scale of the
-two products' absolute sums); the split form may not be worse than 2x the f32 form's largest such error."""
+Linear(dH, n m)) in every product mode (traj_knet_set_fc2_mode): the f32 matrix-core form (0) and the three-term
+bf16 forms (1, 2 = default), each against a float64 evaluation of the same weights and inputs.  Bar: a float32
+GEMM's accuracy, |err| <= 1e-6 x (|b| + |W2b| relu(|W2a| |x2| + |b2a|)) elementwise (the f32 rounding scale of the
+two products' absolute sums); the three-term form may not be worse than 2x the f32 form's largest such error, and
+its two organizations (every wave splitting the tile, or the tile split once into LDS planes) agree bit for bit."""
 import ctypes as C
 
 import numpy as np
@@ -25,7 +26,7 @@ def _model(dev, out_mult, seed=3):
     return K, model
 
 
-def _fc2(K, model, x2, mode, packed=False):
+def _fc2(K, model, x2, mode):
     from trajectory_generation_amd import _lib
     L = _lib.lib()
     net = K.net_struct(model)
@@ -34,16 +35,8 @@ def _fc2(K, model, x2, mode, packed=False):
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     prev = L.traj_knet_set_fc2_mode(mode)
     try:
-        if packed:
-            nb = L.traj_knet_packed_bytes(C.byref(net))
-            pk = torch.empty(nb // 4, dtype=torch.float32, device=x2.device)
-            _lib.check(L.traj_knet_pack_f32(C.byref(net), C.c_void_p(pk.data_ptr()), nb, st), "traj_knet_pack_f32")
-            _lib.check(L.traj_knet_fc2_packed_f32(C.byref(net), C.c_void_p(pk.data_ptr()), B, C.c_void_p(x2.data_ptr()),
-                                                  C.c_void_p(ws.data_ptr()), ws.numel() * 4, st),
-                       "traj_knet_fc2_packed_f32")
-        else:
-            _lib.check(L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()),
-                                           ws.numel() * 4, st), "traj_knet_fc2_f32")
+        _lib.check(L.traj_knet_fc2_f32(C.byref(net), B, C.c_void_p(x2.data_ptr()), C.c_void_p(ws.data_ptr()),
+                                       ws.numel() * 4, st), "traj_knet_fc2_f32")
     finally:
         L.traj_knet_set_fc2_mode(prev)
     torch.cuda.synchronize()
@@ -70,28 +63,21 @@ def test_fc2_modes_vs_float64(gpu, out_mult, B):
     hid = np.maximum(xd @ Wa.T + ba, 0.0)
     ref = hid @ Wb.T + bb
     scale = np.abs(bb) + np.maximum(np.abs(xd) @ np.abs(Wa).T + np.abs(ba), 0.0) @ np.abs(Wb).T
-    errs = {}
-    outs = {}
-    for mode, packed in ((0, False), (1, False), (1, True), (0, True), (2, True), (3, True)):
-        out = _fc2(K, model, x2, mode, packed)
+    errs, outs = {}, {}
+    for mode in (0, 1, 2):
+        out = _fc2(K, model, x2, mode)
         assert np.isfinite(out).all()
         rel = np.abs(out - ref) / scale
-        assert rel.max() <= 1e-6, (mode, packed, rel.max())
-        errs[mode, packed] = rel.max()
-        outs[mode, packed] = out
-    assert errs[1, False] <= 2.0 * errs[0, False] + 1e-7, errs
-    # the weight split once at pack time or in every workgroup: the same terms, the same sums
-    np.testing.assert_array_equal(outs[1, True], outs[1, False])
-    np.testing.assert_array_equal(outs[0, True], outs[0, False])
-    # the x2 tile split once per workgroup into LDS planes (mode 2): the same terms in the same order
-    np.testing.assert_array_equal(outs[2, True], outs[1, True])
-    np.testing.assert_array_equal(outs[3, True], outs[1, True])
+        assert rel.max() <= 1e-6, (mode, rel.max())
+        errs[mode], outs[mode] = rel.max(), out
+    assert errs[2] <= 2.0 * errs[0] + 1e-7, errs
+    np.testing.assert_array_equal(outs[1], outs[2])
 
 
 def test_fc2_mode_switch(gpu):
     from trajectory_generation_amd import _lib
     L = _lib.lib()
-    assert L.traj_knet_set_fc2_mode(4) == -1 and L.traj_knet_set_fc2_mode(-1) == -1
+    assert L.traj_knet_set_fc2_mode(3) == -1 and L.traj_knet_set_fc2_mode(-1) == -1
     prev = L.traj_knet_set_fc2_mode(0)
-    assert prev in (0, 1, 2, 3)
+    assert prev == 2   # the default: the three-term form, tile split once per workgroup
     assert L.traj_knet_set_fc2_mode(prev) == 0

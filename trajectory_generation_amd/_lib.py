@@ -132,7 +132,6 @@ _SIGS = {
     "traj_knet_fc2_workspace_bytes": (C.c_size_t, [C.POINTER(KnetNet), C.c_int]),
     "traj_knet_fc2_f32": (C.c_int, [C.POINTER(KnetNet), C.c_int, _V, _V, C.c_size_t, _V]),
     "traj_knet_set_fc2_mode": (C.c_int, [C.c_int]),
-    "traj_knet_fc2_packed_f32": (C.c_int, [C.POINTER(KnetNet), _V, C.c_int, _V, _V, C.c_size_t, _V]),
     "traj_knet_back_f32": (C.c_int, [C.POINTER(KnetNet), _V, C.c_int, _V, _V, _V, _V, _V, _V, _V, C.c_int,
                                      C.c_int, _V, _V]),
     "traj_knet_back_front_f32": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(KnetLimits), C.c_float,

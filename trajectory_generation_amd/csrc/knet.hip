@@ -220,11 +220,9 @@ struct KNet {
 __host__ __device__ inline int k4_(int K) { return ((K + 63) / 64) * 16; }
 
 // Packed-buffer offsets (in floats) of the eleven matrices, in the order of traj_knet_net.
-// off[11]: FC2.0's weight as three bf16 planes (hi, mid, lo; row-major [d_fc2h][2H] each) for knet_fc2x_kernel; off[12]:
-// the end.
 struct PackPlan {
     int N[11], K[11];
-    size_t off[13];
+    size_t off[12];
 };
 static PackPlan pack_plan(const traj_knet_net* w) {
     PackPlan pl{};
@@ -237,7 +235,6 @@ static PackPlan pack_plan(const traj_knet_net* w) {
         pl.K[i] = K[i];
         pl.off[i + 1] = pl.off[i] + (size_t)4 * k4_(K[i]) * N[i];
     }
-    pl.off[12] = pl.off[11] + (size_t)3 * w->d_fc2h * (2 * H) / 2;   // bf16 planes, in floats
     return pl;
 }
 
@@ -693,17 +690,6 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m
     }
 }
 
-// FC2.0's weight [n = d_fc2h x 2H] into the three planes of the packed buffer (knet_fc2x_kernel<NT, true>)
-__global__ void knet_split_kernel(const float* __restrict__ W, long long n, __bf16* __restrict__ Pl) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    __bf16 h, m, l;
-    split3(W[i], h, m, l);
-    Pl[i] = h;
-    Pl[n + i] = m;
-    Pl[2 * n + i] = l;
-}
-
 __device__ __forceinline__ void split3(const float4& a, const float4& b, bf16x8& h, bf16x8& m, bf16x8& l) {
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     split3(v, h, m, l);
@@ -722,11 +708,13 @@ __device__ __forceinline__ f32x4 mfma6(const bf16x8& ah, const bf16x8& am, const
 
 // The three-term kernels' second half: relu(hidT + b2a) in the accumulators, the second product on the bf16 matrix
 // cores (B = the accumulators, A = W2b split in registers), the four waves' partials added in wave order through LDS
-// (s_red: 4 x 32 x F2_RS floats, free once every wave is past its reads of the tile), part[slab][b][0:32] written.
-template <int NT>
-__device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][4], const float* __restrict__ b2a,
+// (s_red: 4 x 32 x (16 BT + 4) floats, free once every wave is past its reads of the tile), part[slab][b][0:32]
+// written.  BT: 16-sequence tiles per workgroup.
+template <int NT, int BT = 4>
+__device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][BT], const float* __restrict__ b2a,
                                               const float* __restrict__ W2b, int dH, int nout, int hw0, int B, int b0,
                                               int slab, float* s_red, float* __restrict__ part) {
+    constexpr int RS = 16 * BT + 4;   // (F2_RS at BT = 4)
     const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
     // relu(hidT + b2a) in place (register q of lane (g, r) in tile (ht, bt): unit hw0 + 16 ht + 4 g + q, sequence
     // b0 + 16 bt + r)
@@ -734,7 +722,7 @@ __device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][4], const float* 
     for (int ht = 0; ht < NT; ++ht) {
         const float4 bias = *reinterpret_cast<const float4*>(b2a + hw0 + 16 * ht + 4 * g);
 #pragma unroll
-        for (int bt = 0; bt < 4; ++bt)
+        for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
             for (int q = 0; q < 4; ++q) acc[ht][bt][q] = fmaxf(__fadd_rn(acc[ht][bt][q], f4c(bias, q)), 0.0f);
     }
@@ -743,11 +731,11 @@ __device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][4], const float* 
     const float* pb[2] = {W2b + (size_t)min(r, nout - 1) * dH + hw0 + 4 * g,
                           W2b + (size_t)min(16 + r, nout - 1) * dH + hw0 + 4 * g};
     const float mk[2] = {m0, m1};
-    f32x4 o[2][4];
+    f32x4 o[2][BT];
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int bt = 0; bt < 4; ++bt) o[jt][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int bt = 0; bt < BT; ++bt) o[jt][bt] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
     for (int s = 0; s < (NT + 1) / 2; ++s) {
         constexpr float z = 0.0f;
@@ -762,7 +750,7 @@ __device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][4], const float* 
             split3(v, wh[jt], wm[jt], wl[jt]);
         }
 #pragma unroll
-        for (int bt = 0; bt < 4; ++bt) {
+        for (int bt = 0; bt < BT; ++bt) {
             float v[8];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -776,36 +764,35 @@ __device__ __forceinline__ void fc2x_epilogue(f32x4 (&acc)[NT][4], const float* 
         }
     }
     __syncthreads();   // every wave is done with the tile in LDS
-    float* red = s_red + w * 32 * F2_RS;
+    float* red = s_red + w * 32 * RS;
 #pragma unroll
     for (int jt = 0; jt < 2; ++jt)
 #pragma unroll
-        for (int bt = 0; bt < 4; ++bt)
+        for (int bt = 0; bt < BT; ++bt)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) red[(16 * jt + 4 * g + q) * F2_RS + 16 * bt + r] = o[jt][bt][q];
+            for (int q = 0; q < 4; ++q) red[(16 * jt + 4 * g + q) * RS + 16 * bt + r] = o[jt][bt][q];
     __syncthreads();
-    {   // thread t: sequence t >> 2, outputs 8 (t & 3) .. + 7; waves added in order
-        const int bb = t >> 2, j0 = 8 * (t & 3);
-        float v[8];
+    {   // thread t: sequence t / TPS, outputs JW (t % TPS) .. + JW - 1; waves added in order
+        constexpr int SEQ = 16 * BT, TPS = 256 / SEQ, JW = 32 / TPS;
+        const int bb = t / TPS, j0 = JW * (t % TPS);
+        float v[JW];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-            const float* p0 = s_red + (j0 + jj) * F2_RS + bb;
-            v[jj] = __fadd_rn(__fadd_rn(__fadd_rn(p0[0], p0[32 * F2_RS]), p0[64 * F2_RS]), p0[96 * F2_RS]);
+        for (int jj = 0; jj < JW; ++jj) {
+            const float* p0 = s_red + (j0 + jj) * RS + bb;
+            v[jj] = __fadd_rn(__fadd_rn(__fadd_rn(p0[0], p0[32 * RS]), p0[64 * RS]), p0[96 * RS]);
         }
         if (b0 + bb < B) {
             float4* dst = reinterpret_cast<float4*>(part + ((size_t)slab * B + b0 + bb) * 32 + j0);
-            dst[0] = make_float4(v[0], v[1], v[2], v[3]);
-            dst[1] = make_float4(v[4], v[5], v[6], v[7]);
+#pragma unroll
+            for (int k = 0; k < JW / 4; ++k) dst[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
         }
     }
 }
 
-// PRE: A from the packed buffer's three planes of W2a (split once at pack time; one 16-byte load per plane), else
-// W2a split in registers as it streams in.
-template <int NT, bool PRE>
+template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2x_kernel(
-    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const __bf16* __restrict__ Wp,
-    const float* __restrict__ b2a, const float* __restrict__ W2b, int nout, float* __restrict__ part) {
+    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const float* __restrict__ b2a,
+    const float* __restrict__ W2b, int nout, float* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) float s_t[F2_BT * F2_LD];   // x2 tile, then the wave partials
     constexpr int HS = 64 * NT;
     const int nslab = dH / HS, nbb = (B + F2_BT - 1) / F2_BT;
@@ -829,22 +816,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         *reinterpret_cast<float4*>(s_t + row * F2_LD + 4 * c4) = reinterpret_cast<const float4*>(x2 + (size_t)bsrc * K)[c4];
     }
     const float* pa = W2a + (size_t)(hw0 + r) * K + 8 * g;   // h-tile ht: + 16 ht K; K step c: + 32 c
-    const size_t pln = (size_t)dH * K;                        // PRE: plane stride
-    const __bf16* pp = Wp + (size_t)(hw0 + r) * K + 8 * g;
     constexpr int NC = K / 32;
-    float4 an[PRE ? 1 : NT][2];
-    bf16x8 apn[PRE ? NT : 1][3];
+    float4 an[NT][2];
     auto load_a = [&](int c) {
 #pragma unroll
         for (int ht = 0; ht < NT; ++ht) {
-            if constexpr (PRE) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    apn[ht][q] = *reinterpret_cast<const bf16x8*>(pp + q * pln + (size_t)16 * ht * K + 32 * c);
-            } else {
-                an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c);
-                an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c + 4);
-            }
+            an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c);
+            an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c + 4);
         }
     };
     load_a(0);
@@ -858,15 +836,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (int c = 0; c < NC; ++c) {
         bf16x8 ah[NT], am[NT], al[NT];
 #pragma unroll
-        for (int ht = 0; ht < NT; ++ht) {
-            if constexpr (PRE) {
-                ah[ht] = apn[ht][0];
-                am[ht] = apn[ht][1];
-                al[ht] = apn[ht][2];
-            } else {
-                split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
-            }
-        }
+        for (int ht = 0; ht < NT; ++ht) split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
         if (c + 1 < NC) load_a(c + 1);
 #pragma unroll
         for (int bt = 0; bt < 4; ++bt) {
@@ -886,10 +856,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 constexpr int F2_HK = KH;            // K columns per half
 constexpr int F2_BLD = F2_HK + 8;    // bf16 per LDS plane row (272 B: rows 4 banks apart)
 
-template <int NT, bool PRE>
+template <int NT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void knet_fc2y_kernel(
-    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const __bf16* __restrict__ Wp,
-    const float* __restrict__ b2a, const float* __restrict__ W2b, int nout, float* __restrict__ part) {
+    int B, int dH, const float* __restrict__ x2, const float* __restrict__ W2a, const float* __restrict__ b2a,
+    const float* __restrict__ W2b, int nout, float* __restrict__ part) {
     constexpr int PL = F2_BT * F2_BLD;
     __shared__ __attribute__((aligned(16))) __bf16 s_b[3 * PL];   // one K half of the tile: hi, mid, lo planes
     static_assert(4 * 32 * F2_RS * sizeof(float) <= sizeof(s_b), "partials fit the planes");
@@ -908,26 +878,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const int t = threadIdx.x, w = t >> 6, l = t & 63, g = l >> 4, r = l & 15;
     const int b0 = bblk * F2_BT, hw0 = slab * HS + 16 * NT * w;
     constexpr int K = 2 * KH, NC = K / 32;
-#ifndef TRAJ_FC2_EXP
-#define TRAJ_FC2_EXP 0   // timing experiments only (wrong results): 1 = every slab reads slab 0's W2a rows, 2 = K step
-#endif                   // 0's A for every K step
-    const float* pa = W2a + (size_t)((TRAJ_FC2_EXP == 1 ? 16 * NT * w : hw0) + r) * K + 8 * g;
-    const size_t pln = (size_t)dH * K;
-    const __bf16* pp = Wp + (size_t)(hw0 + r) * K + 8 * g;
-    float4 an[PRE ? 1 : NT][2];
-    bf16x8 apn[PRE ? NT : 1][3];
+    const float* pa = W2a + (size_t)(hw0 + r) * K + 8 * g;
+    float4 an[NT][2];
     auto load_a = [&](int c) {
-        if (TRAJ_FC2_EXP == 2 && c > 0) return;
 #pragma unroll
         for (int ht = 0; ht < NT; ++ht) {
-            if constexpr (PRE) {
-#pragma unroll
-                for (int q = 0; q < 3; ++q)
-                    apn[ht][q] = *reinterpret_cast<const bf16x8*>(pp + q * pln + (size_t)16 * ht * K + 32 * c);
-            } else {
-                an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c);
-                an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c + 4);
-            }
+            an[ht][0] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c);
+            an[ht][1] = *reinterpret_cast<const float4*>(pa + (size_t)16 * ht * K + 32 * c + 4);
         }
     };
     // half hf of the tile, split: thread t takes float4 q = t + 256 it (row q / 32, columns hf 128 + 4 (q % 32) .. + 3)
@@ -971,15 +928,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         }
         bf16x8 ah[NT], am[NT], al[NT];
 #pragma unroll
-        for (int ht = 0; ht < NT; ++ht) {
-            if constexpr (PRE) {
-                ah[ht] = apn[ht][0];
-                am[ht] = apn[ht][1];
-                al[ht] = apn[ht][2];
-            } else {
-                split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
-            }
-        }
+        for (int ht = 0; ht < NT; ++ht) split3(an[ht][0], an[ht][1], ah[ht], am[ht], al[ht]);
         if (c + 1 < NC) load_a(c + 1);
         const int cc = c & (NC / 2 - 1);
 #pragma unroll
@@ -1358,32 +1307,18 @@ inline int nblk(long long n, int t) { return (int)((n + t - 1) / t); }
 }  // namespace
 
 // traj_knet_set_fc2_mode: 2 = knet_fc2y_kernel (three-term bf16 operands, the tile split once per workgroup; the
-// default), 1 = knet_fc2x_kernel (the same terms, every wave splitting the tile), 3 = knet_fc2y_kernel with W2a's planes
-// from the packed buffer, 0 = knet_fc2_kernel (f32).  Modes 1-3 give identical results.
+// default), 1 = knet_fc2x_kernel (the same terms and sums, every wave splitting the tile), 0 = knet_fc2_kernel (f32).
 static std::atomic<int> g_fc2_mode{2};
 
-// FC2 launch: packed != NULL takes W2a's bf16 planes from the packed buffer (traj_knet_fc2_packed_f32)
-static int fc2_launch(const traj_knet_net* net, const float* packed, int B, const float* x2, float* ws, void* stream) {
+// FC2 launch in the mode of traj_knet_set_fc2_mode
+static int fc2_launch(const traj_knet_net* net, int B, const float* x2, float* ws, void* stream) {
     const int hs = fc2_slab(net->d_fc2h), nslab = net->d_fc2h / hs, nbb = nblk(B, F2_BT);
     const int mode = g_fc2_mode.load(std::memory_order_relaxed);
-    const bool split = mode != 0;
-    const __bf16* wp = packed ? reinterpret_cast<const __bf16*>(packed + pack_plan(net).off[11]) : nullptr;
-    if (mode >= 2) {
-        auto ky = hs == 320 ? (mode == 3 && wp ? knet_fc2y_kernel<5, true> : knet_fc2y_kernel<5, false>)
-                            : (mode == 3 && wp ? knet_fc2y_kernel<4, true> : knet_fc2y_kernel<4, false>);
-        hipLaunchKernelGGL(ky, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w,
-                           wp, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
-        return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
-    }
-    auto kern = hs == 320 ? (wp ? knet_fc2x_kernel<5, true> : knet_fc2x_kernel<5, false>)
-                          : (wp ? knet_fc2x_kernel<4, true> : knet_fc2x_kernel<4, false>);
-    if (split)
-        hipLaunchKernelGGL(kern, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2,
-                           net->fc2a_w, wp, net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
-    else
-        hipLaunchKernelGGL(hs == 320 ? knet_fc2_kernel<5> : knet_fc2_kernel<4>, dim3(nslab * nbb), dim3(256), 0,
-                           (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w, net->fc2a_b, net->fc2b_w,
-                           net->n * net->m, ws);
+    auto kern = mode == 2 ? (hs == 320 ? knet_fc2y_kernel<5> : knet_fc2y_kernel<4>)
+              : mode == 1 ? (hs == 320 ? knet_fc2x_kernel<5> : knet_fc2x_kernel<4>)
+                          : (hs == 320 ? knet_fc2_kernel<5> : knet_fc2_kernel<4>);
+    hipLaunchKernelGGL(kern, dim3(nslab * nbb), dim3(256), 0, (hipStream_t)stream, B, net->d_fc2h, x2, net->fc2a_w,
+                       net->fc2a_b, net->fc2b_w, net->n * net->m, ws);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
@@ -1472,14 +1407,14 @@ static KNet knet_args(const traj_knet_net* w, const float* packed) {
 
 size_t traj_knet_packed_bytes(const traj_knet_net* net) {
     if (!knet_ok(net)) return 0;
-    return pack_plan(net).off[12] * sizeof(float);
+    return pack_plan(net).off[11] * sizeof(float);
 }
 
 int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, void* stream) {
     if (!net || !packed) return TRAJ_E_ARG;
     if (!knet_ok(net)) return TRAJ_E_UNSUPPORTED;
     const PackPlan pl = pack_plan(net);
-    if (bytes < pl.off[12] * sizeof(float) || ((uintptr_t)packed & 15)) return TRAJ_E_ARG;
+    if (bytes < pl.off[11] * sizeof(float) || ((uintptr_t)packed & 15)) return TRAJ_E_ARG;
     const float* W[11] = {net->fc5_w, net->gru_q_wih, net->gru_q_whh, net->gru_sigma_wih, net->gru_sigma_whh,
                           net->fc1_w, net->fc7_w,     net->gru_s_wih, net->gru_s_whh,     net->fc3_w,
                           net->fc4_w};
@@ -1488,9 +1423,6 @@ int traj_knet_pack_f32(const traj_knet_net* net, float* packed, size_t bytes, vo
         hipLaunchKernelGGL(knet_pack_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, W[i], pl.N[i],
                            pl.K[i], packed + pl.off[i]);
     }
-    const long long n2 = (long long)net->d_fc2h * 2 * net->hidden;
-    hipLaunchKernelGGL(knet_split_kernel, dim3(nblk(n2, 256)), dim3(256), 0, (hipStream_t)stream, net->fc2a_w, n2,
-                       reinterpret_cast<__bf16*>(packed + pl.off[11]));
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
@@ -1528,23 +1460,11 @@ int traj_knet_fc2_f32(const traj_knet_net* net, int B, const float* x2, float* w
         ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2a_b & 15) || ((uintptr_t)net->fc2b_w & 15))
         return TRAJ_E_ARG;
     const int hs = fc2_slab(net->d_fc2h), nslab = net->d_fc2h / hs, nbb = nblk(B, F2_BT);
-    return fc2_launch(net, nullptr, B, x2, ws, stream);
-}
-
-int traj_knet_fc2_packed_f32(const traj_knet_net* net, const float* packed, int B, const float* x2, float* ws,
-                             size_t ws_bytes, void* stream) {
-    if (B < 0) return TRAJ_E_ARG;
-    if (!knet_ok(net)) return net ? TRAJ_E_UNSUPPORTED : TRAJ_E_ARG;
-    if (B == 0) return TRAJ_OK;
-    if (!packed || ((uintptr_t)packed & 15) || !x2 || !ws || ws_bytes < traj_knet_fc2_workspace_bytes(net, B) ||
-        ((uintptr_t)x2 & 15) || ((uintptr_t)net->fc2a_w & 15) || ((uintptr_t)net->fc2a_b & 15) ||
-        ((uintptr_t)net->fc2b_w & 15))
-        return TRAJ_E_ARG;
-    return fc2_launch(net, packed, B, x2, ws, stream);
+    return fc2_launch(net, B, x2, ws, stream);
 }
 
 int traj_knet_set_fc2_mode(int mode) {
-    if (mode < 0 || mode > 3) return -1;
+    if (mode < 0 || mode > 2) return -1;
     return g_fc2_mode.exchange(mode);
 }
 

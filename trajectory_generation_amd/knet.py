@@ -13,8 +13,9 @@ its checkpoints load unchanged.  What runs on the device per step (kalman_net.py
 
 ``KNetSequenceRunner`` captures one whole step in a HIP graph and replays it T times; its fused mode
 (the throughput path) runs a step as ``traj_knet_front_f32`` (prior + FC5 + the three GRU cells + FC1/FC7
-for four sequences per workgroup), ``traj_knet_fc2_packed_f32`` (FC2 on the bf16 matrix cores with every
-f32 operand carried as three bf16 terms -- f32-accurate sums -- its [B, 10240] hidden activation kept on chip) and ``traj_knet_back_f32`` (FC3 + FC4 + posterior update), with back(t)
+for four sequences per workgroup), ``traj_knet_fc2_f32`` (FC2 on the bf16 matrix cores with every
+f32 operand carried as three bf16 terms -- f32-accurate sums -- its [B, 10240] hidden activation kept
+on chip) and ``traj_knet_back_f32`` (FC3 + FC4 + posterior update), with back(t)
 and front(t + 1) fused into one launch (``traj_knet_back_front_f32``), and captures all T steps in one
 graph.
 There is no CPU path: the ops raise without the HIP library or a GPU.
@@ -455,8 +456,8 @@ class KNetSequenceRunner:
                     C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, row("post", m),
                     ucol(0), 2 * T, T, ycol(0), n * T, T, *norm, row("hQ", H), row("hSig", H), row("hS", H),
                     row("prior", m), row("dy", n), row("x2", 2 * H), _stream()), "traj_knet_front_f32")
-            _lib.check(L.traj_knet_fc2_packed_f32(net, pk, Bg, row("x2", 2 * H), _p(ws), ws.numel() * 4, _stream()),
-                       "traj_knet_fc2_packed_f32")
+            _lib.check(L.traj_knet_fc2_f32(net, Bg, row("x2", 2 * H), _p(ws), ws.numel() * 4, _stream()),
+                       "traj_knet_fc2_f32")
             if t + 1 < steps and self.merge:
                 _lib.check(L.traj_knet_back_front_f32(
                     C.byref(S["p"]), C.byref(S["lim"]), float(md.sys.Ts), net, pk, Bg, _p(ws), ocol(t), m * T, T,

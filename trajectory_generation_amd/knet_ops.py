@@ -295,8 +295,7 @@ def step(y: torch.Tensor, u: torch.Tensor, x_post: torch.Tensor, h_q: torch.Tens
                                      C.byref(net), _p(pk), B, _p(post), _p(uu), 2, 1, _p(yy), n, 1,
                                      *[_p(t) for t in nrm], _p(hq), _p(hsig), _p(hs), _p(prior_), _p(dy), _p(x2), st),
                "trajknet::step (front)")
-    _lib.check(L.traj_knet_fc2_packed_f32(C.byref(net), _p(pk), B, _p(x2), _p(ws), ws.numel() * 4, st),
-               "trajknet::step (fc2)")
+    _lib.check(L.traj_knet_fc2_f32(C.byref(net), B, _p(x2), _p(ws), ws.numel() * 4, st), "trajknet::step (fc2)")
     _lib.check(L.traj_knet_back_f32(C.byref(net), _p(pk), B, _p(x2), _p(ws), _p(prior_), _p(dy), _p(hsig), _p(out),
                                     None, 0, 0, _p(KG), st), "trajknet::step (back)")
     return out, hq, hsig, hs, KG
