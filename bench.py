@@ -183,6 +183,8 @@ def cpu_baseline_config1(N, Ts, x0, u0, vref, path, T):
 # KalmanNet (BASELINE.json configs[4]): 1024 sequences x 200 steps, Ts = 0.01, float32
 KNET_FLOP_PER_SEQ_STEP = 2 * 3_178_373     # MACs of one gain-network step x 2
 FP32_MFMA_PEAK_TFS = 157.3                 # MI355X dense fp32 matrix peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFS = 2500.0                # MI355X dense bf16 matrix peak (the same guide; 2:1-sparse figures excluded)
+FC2_TERM_PRODUCTS = 6                      # three-term bf16 form: bf16 MFMA products per f32 product
 # fixed clamp limits for the tools' synthetic-input KalmanNet runs (the bench derives its own from data)
 KNET_LIMITS = {"x_min": -5.0, "x_max": 40.0, "y_min": -6.0, "y_max": 6.0, "phi_min": -3.2, "phi_max": 3.2,
                "vx_min": 0.0, "vx_max": 3.0, "vy_min": -1.0, "vy_max": 1.0, "omega_min": -6.0, "omega_max": 6.0}
@@ -202,8 +204,10 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
     emitter's closed loop + the reference's measurement noise), normalization and clamp limits from a
     separate train draw, seeded-init weights of the reference architecture, all T fused steps replayed
     as one HIP graph.  The same run's posteriors give KalmanNet's MSE (test_vehicle.py:143-158), set
-    beside the EKF baseline's on the same measurements.  The roofline object is the dominant kernel's
-    (knet_fc2_kernel, f32 MFMA), timed with events over standalone launches on the same data."""
+    beside the EKF baseline's on the same measurements.  The roofline object is the dominant kernel's (the FC2
+    launch: by default knet_fc2y_kernel, f32 operands as three bf16 terms on the bf16 matrix cores), timed with
+    events over standalone launches on the same data; its peak is the bf16 MFMA peak over the six term products
+    one f32 product takes, with the f32 MFMA peak beside it."""
     from trajectory_generation_amd import knet as K
     from trajectory_generation_amd import knet_eval as KE
     Ts = 0.01
@@ -253,13 +257,24 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
     fc2_ms = e0.elapsed_time(e1) / reps
     fc2_flop = knet_fc2_flop(B, model)
     fc2_tfs = fc2_flop / (fc2_ms * 1e-3) / 1e12
+    fc2_mode = L.traj_knet_set_fc2_mode(0)   # (query: set and restore)
+    L.traj_knet_set_fc2_mode(fc2_mode)
+    if fc2_mode == 0:
+        fc2_kernel, fc2_peak = "knet_fc2_kernel<5>", FP32_MFMA_PEAK_TFS
+        fc2_peak_note = "f32 MFMA (v_mfma_f32_16x16x4_f32) dense peak"
+    else:
+        fc2_kernel = "knet_fc2y_kernel<5>" if fc2_mode == 2 else "knet_fc2x_kernel<5>"
+        fc2_peak = BF16_MFMA_PEAK_TFS / FC2_TERM_PRODUCTS
+        fc2_peak_note = ("f32 FLOP/s ceiling of the three-term form: the dense bf16 MFMA peak / 6 bf16 products per "
+                         "f32 product (f32-accurate sums; DESIGN.md 6d)")
     traffic = None
     if os.path.exists(traffic_json):
         try:
             with open(traffic_json) as f:
                 tj = json.load(f)
             if tj.get("batch") == B:
-                traffic = tj.get("hbm_bytes_per_launch", {}).get("knet_fc2_kernel")
+                hb = tj.get("hbm_bytes_per_launch", {})
+                traffic = hb.get("knet_fc2", hb.get("knet_fc2_kernel"))
         except (OSError, ValueError):
             traffic = None
     dt_step_graph = timed(fused=False)   # module-level step (per-layer launches), one-step graph
@@ -278,9 +293,11 @@ def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
                        + (f"from {os.path.basename(weights)}" if weights else
                           "are the seeded init (no trained weights ship; see 'mse_trained')")
                        + ", the EKF is the build's baseline (f2)",
-           "roofline": {"bound": "mfma", "achieved": fc2_tfs, "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": fc2_tfs / FP32_MFMA_PEAK_TFS, "traffic": traffic,
-                        "kernel": "knet_fc2_kernel<5> (FC2: Linear 256->10240, ReLU, Linear 10240->30)",
+           "roofline": {"bound": "mfma", "achieved": fc2_tfs, "peak": fc2_peak, "unit": "TFLOP/s",
+                        "frac": fc2_tfs / fc2_peak, "traffic": traffic,
+                        "kernel": fc2_kernel + " (FC2: Linear 256->10240, ReLU, Linear 10240->30)",
+                        "fc2_mode": fc2_mode, "peak_note": fc2_peak_note,
+                        "f32_mfma_peak": FP32_MFMA_PEAK_TFS, "frac_of_f32_mfma_peak": fc2_tfs / FP32_MFMA_PEAK_TFS,
                         "kernel_ms": fc2_ms, "flop_per_launch": fc2_flop,
                         "traffic_source": os.path.relpath(traffic_json, HERE) if traffic is not None else None,
                         "whole_step": {"achieved": achieved, "frac": achieved / FP32_MFMA_PEAK_TFS,

@@ -1,4 +1,5 @@
-"""Per-launch HBM traffic of knet_fc2_kernel (the KalmanNet step's dominant kernel) from rocprofv3 PMC
+"""Per-launch HBM traffic of the FC2 launch (knet_fc2y_kernel by default, knet_fc2_kernel / knet_fc2x_kernel in the
+other traj_knet_set_fc2_mode modes; the KalmanNet step's dominant kernel) from rocprofv3 PMC
 passes (FETCH_SIZE and WRITE_SIZE in separate runs over tools/knet_bench.py):
 
   python tools/pmc_knet_traffic.py --fetch DIR1 --write DIR2 --batch 1024 --out profiles/traffic_knet_r01.json
@@ -11,7 +12,10 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
+
+FC2 = re.compile(r"knet_fc2[xy]?_kernel")
 
 
 def read(d, name, wgs):
@@ -22,7 +26,7 @@ def read(d, name, wgs):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") != name or "knet_fc2_kernel" not in row.get("Kernel_Name", ""):
+                if row.get("Counter_Name") != name or not FC2.search(row.get("Kernel_Name", "")):
                     continue
                 grid = int(row.get("Grid_Size", "0") or 0)
                 wg = int(row.get("Workgroup_Size", "1") or 1)
@@ -30,7 +34,7 @@ def read(d, name, wgs):
                     continue
                 vals[row.get("Dispatch_Id")] += float(row["Counter_Value"])
     if not vals:
-        raise SystemExit(f"no knet_fc2_kernel dispatch of {wgs} workgroups in {d}")
+        raise SystemExit(f"no FC2 dispatch of {wgs} workgroups in {d}")
     return sum(vals.values()) / len(vals), len(vals)
 
 
@@ -49,8 +53,8 @@ def main():
     # algorithmic bytes: x2 [B, 256] + W2a [10240, 256] + b2a + W2b [30, 10240] read once, partials written
     alg = 4 * (a.batch * 256 + 10240 * 256 + 10240 + 30 * 10240 + 32 * a.batch * 32)
     res = {"batch": a.batch, "dispatches": {"fetch": nf, "write": nw},
-           "fetch_bytes_per_launch": {"knet_fc2_kernel": fb}, "write_bytes_per_launch": {"knet_fc2_kernel": wb},
-           "hbm_bytes_per_launch": {"knet_fc2_kernel": fb + wb}, "algorithmic_bytes_per_launch": alg,
+           "fetch_bytes_per_launch": {"knet_fc2": fb}, "write_bytes_per_launch": {"knet_fc2": wb},
+           "hbm_bytes_per_launch": {"knet_fc2": fb + wb}, "algorithmic_bytes_per_launch": alg,
            "note": "FETCH_SIZE x2 (gfx950 correction), KiB -> bytes; the weights (12 MB) are re-read every step "
                    "from the Infinity Cache / HBM, the hidden activation never leaves the chip"}
     with open(a.out, "w") as fh:
