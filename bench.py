@@ -197,7 +197,7 @@ def knet_fc2_flop(B, model):
 
 
 def knet_measure(dev, B=1024, T=200, cpu=True, cpu_T=50,
-                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r03.json"), weights=None,
+                 traffic_json=os.path.join(HERE, "profiles", "traffic_knet_r05.json"), weights=None,
                  trained_json=os.path.join(HERE, "profiles", "r03_knet_trained_mse.json")):
     """Sequences/s of KalmanNet inference (BASELINE.json configs[4]) on 1024 noisy closed-loop
     trajectories x 200 steps at Ts = 0.01 generated on the GPU (knet_eval.make_sequences: the dataset
@@ -595,13 +595,13 @@ def parse_args(argv=None):
                     help="skip the one-trajectory measurement (configs[0]: drop-in per call, fused B=1, oracle 1 thread)")
     ap.add_argument("--per-step", action="store_true",
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r04.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r05.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
-    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r04.json"),
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r05.json"),
                     help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
-    ap.add_argument("--stall-json", default=os.path.join(HERE, "profiles", "r04_pmc_stall.json"),
+    ap.add_argument("--stall-json", default=os.path.join(HERE, "profiles", "r05_pmc_stall.json"),
                     help="SQ wave-cycle counters of the fused launch (tools/pmc_stall.sh / pmc_stall.py)")
-    ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r03.json"),
+    ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r05.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
     ap.add_argument("--knet-weights", default=None,
                     help="safetensors of trained KalmanNet weights (tools/knet_train_eval.py --save) for configs[4]")
@@ -614,7 +614,16 @@ def parse_args(argv=None):
                     help="skip the reference-semantics (cold-start) pass reported as 'cold'")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds before a process-group rendezvous or collective gives up (N > 1)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    # the profiles of another horizon (config 3's N = 40: traffic_r05_n40.json, sq_f64_r05_n40.json) when the
+    # defaults are in use and such a file exists
+    if args.horizon != 20:
+        for k in ("traffic_json", "issue_json"):
+            v = getattr(args, k)
+            alt = v[:-5] + f"_n{args.horizon}.json"
+            if v == ap.get_default(k) and os.path.exists(alt):
+                setattr(args, k, alt)
+    return args
 
 
 def main(argv=None, ops_factory=None, backend=None):

@@ -18,8 +18,8 @@
 #   trace       rocprofv3 --kernel-trace --stats of the driver's command + the solve dispatches
 #               (tools/trace_dispatches.py)                                    -> gpurun_out/$TAG_kt/, $TAG_dispatches.json
 #   tiers       horizon tiers: batch (B = 1024) and drop-in per-call times (tools/horizon_tiers.py) -> $TAG_tiers.json
-#   ktraffic    PMC FETCH_SIZE / WRITE_SIZE passes over the KalmanNet leg (tools/knet_bench.py): the FC2 launch's
-#               HBM bytes (tools/pmc_knet_traffic.py)                          -> gpurun_out/$TAG_traffic_knet.json
+#   ktraffic    PMC FETCH_SIZE / WRITE_SIZE passes over the FC2 launch alone at B = 1024 in the default mode
+#               (tools/knet_fc2_pmc.py): its HBM bytes (tools/pmc_knet_traffic.py) -> gpurun_out/$TAG_traffic_knet.json
 #   kfc2        PMC passes over FC2 alone in each product mode (tools/pmc_knet_fc2.sh) -> gpurun_out/$TAG_fc2_m*/
 #   ab          A/B of library variants (VARIANTS="v1 v2" under trajectory_generation_amd/_variants/<v>/, built by
 #               tools/build_variant.sh) against the in-tree build, REPS rounds of CFGS "steps:waves" configurations
@@ -96,10 +96,10 @@ for step in "$@"; do
             || { tail -5 $O/${TAG}_tiers.err; exit 1; }
         cat $O/${TAG}_tiers.json ;;
     ktraffic)
-        timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/${TAG}_kfetch -o run --output-format csv -- \
-            python3 tools/knet_bench.py > $O/${TAG}_kfetch.log 2>&1 &&
-        timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/${TAG}_kwrite -o run --output-format csv -- \
-            python3 tools/knet_bench.py > $O/${TAG}_kwrite.log 2>&1 &&
+        timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/${TAG}_kfetch -o run --output-format csv -- \
+            python3 tools/knet_fc2_pmc.py 2 > $O/${TAG}_kfetch.log 2>&1 &&
+        timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/${TAG}_kwrite -o run --output-format csv -- \
+            python3 tools/knet_fc2_pmc.py 2 > $O/${TAG}_kwrite.log 2>&1 &&
         python3 tools/pmc_knet_traffic.py --fetch $O/${TAG}_kfetch --write $O/${TAG}_kwrite --batch 1024 \
             --out $O/${TAG}_traffic_knet.json > /dev/null && echo ok || exit 1 ;;
     kfc2) timeout -k 10 600 tools/pmc_knet_fc2.sh $TAG || exit 1 ;;
