@@ -399,8 +399,8 @@ def _same(a, b):
 
 @pytest.mark.parametrize("N,warm,mode", [(20, 1, 0), (18, 1, 0), (20, 0, 1)])
 def test_fused_three_waves_bit_identical(gpu, N, warm, mode):
-    """The 3-waves-per-SIMD fused instance (capacity 40: 168 VGPRs, compact LDS image; chosen for runs of
-    TRAJ_FUSED_W3_MIN_STEPS or more) equals the 2-wave instance and the per-step launches bit for bit; N = 18
+    """The 3-waves-per-SIMD fused instance (capacity 40: 168 VGPRs, compact LDS image; opt-in since round 5,
+    traj_debug_fused_waves(3)) equals the 2-wave instance and the per-step launches bit for bit; N = 18
     leaves padding rows in the capacity-40 kernel."""
     from trajectory_generation_amd import _lib
     from trajectory_generation_amd.workload import make_workload
@@ -411,7 +411,7 @@ def test_fused_three_waves_bit_identical(gpu, N, warm, mode):
     per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
     runs = {}
     try:
-        for wv in (2, 3, 0):   # forced 2, forced 3, by launch length (200 steps: 3)
+        for wv in (2, 3, 0):   # forced 2, forced 3, by launch length (the default: 2)
             _lib.check(_lib.lib().traj_debug_fused_waves(wv), "traj_debug_fused_waves")
             runs[wv] = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
     finally:

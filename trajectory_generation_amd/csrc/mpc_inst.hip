@@ -28,8 +28,8 @@ int TGMPC_CAT(launch_mpc_, TGMPC_NN)(const KArgs& a, hipStream_t st, int mode) {
 #if TGMPC_NN == 40
         {
             // HIP loads a kernel's code object at its first launch (milliseconds of host time for these): the first
-            // fused launch at this capacity loads BOTH instances, so a later long launch (the 3-wave one, e.g. the
-            // configs[3] dataset leg after a 20-step run) does not pay it inside its own call.  Per device.
+            // fused launch at this capacity loads BOTH instances, so a later launch of the other one (the opt-in
+            // 3-wave instance, traj_debug_fused_waves(3)) does not pay it inside its own call.  Per device.
             static std::atomic<bool> loaded[64];
             int dev = 0;
             if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && !loaded[dev].load()) {

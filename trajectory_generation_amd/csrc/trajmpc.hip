@@ -272,12 +272,13 @@ static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
 static long long* g_dbg = nullptr;  // diagnostics buffer (traj_debug_set_stamps)
 static long long* g_dbg_items = nullptr;  // fused-run item timeline (traj_debug_set_item_stamps)
 static int g_fused_grid = 0;        // traj_debug_fused_grid
-// fused runs of at least this many steps use the 3-waves-per-SIMD kernel (capacity 40): more throughput once
-// the launch is bound by its bulk (bench workload, 200 steps: 14.35 M vs 13.51 M steps/s) but each item's latency
-// grows, and a shorter launch is bound by its heaviest instances' chains of items (20 steps: 10.1 M vs 11.7 M;
-// 100 steps: 10.4 M vs 12.1 M) -- DESIGN.md section 5
+// fused runs of at least this many steps use the 3-waves-per-SIMD kernel (capacity 40; 0 = never).  Round 3 measured
+// it ahead over long launches (200 steps: 14.35 M vs 13.51 M steps/s; behind at 20 and 100 steps, where a launch is
+// bound by its heaviest instances' chains); since round 4's arithmetic work the 2-wave instance matches it there
+// (round 5, 240 steps: 16.26-16.28 M vs 16.32-16.39 M) without its 156 B/lane of scratch, so it runs every launch
+// length and the 3-wave instance is opt-in (traj_debug_fused_waves(3)) -- DESIGN.md section 5
 #ifndef TRAJ_FUSED_W3_MIN_STEPS
-#define TRAJ_FUSED_W3_MIN_STEPS 200
+#define TRAJ_FUSED_W3_MIN_STEPS 0
 #endif
 static int g_fused_waves = 0;       // traj_debug_fused_waves: 0 = by launch length, 2 or 3 = forced
 static int g_spin_limit = 1 << 22;  // traj_debug_spin_limit: polls before a fused hand-off is declared lost
@@ -644,9 +645,10 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.dbg = g_dbg;
     a.nsteps = steps;
     a.fused_grid = g_fused_grid;
-    // kernel instance: capacity 40, 2 waves per SIMD (3 from TRAJ_FUSED_W3_MIN_STEPS steps); capacity 80, one
-    // wave per SIMD (the lean two-wave instance, traj_debug_fused_waves(2), spills at its 256 registers)
-    a.wps = g_fused_waves ? g_fused_waves : (2 * c->N > 64 ? 1 : (steps >= TRAJ_FUSED_W3_MIN_STEPS ? 3 : 2));
+    // kernel instance: capacity 40, 2 waves per SIMD (3 from TRAJ_FUSED_W3_MIN_STEPS steps when that is set); capacity
+    // 80, one wave per SIMD (the lean two-wave instance, traj_debug_fused_waves(2), spills at its 256 registers)
+    constexpr int w3_min = TRAJ_FUSED_W3_MIN_STEPS;
+    a.wps = g_fused_waves ? g_fused_waves : (2 * c->N > 64 ? 1 : ((w3_min > 0 && steps >= w3_min) ? 3 : 2));
     a.spin_limit = g_spin_limit;
     a.dbg_items = g_dbg_items;
     carve_workspace(a, workspace, B, c->N);
