@@ -80,6 +80,10 @@
 #ifndef TGMPC_PMUL_W2
 #define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
 #endif
+#ifndef TGMPC_KMC
+#define TGMPC_KMC 8            // independent FMA chains of the ADMM mat-vec (K^-1 v): 4 or 8 (8: +0.7 % at the
+                               // driver's command in 3 interleaved pairs, round 5; the chains are latency-bound)
+#endif
 #ifndef TGMPC_KCH80
 #define TGMPC_KCH80 16         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec
 #endif
@@ -1074,15 +1078,21 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
         };
         double Krow[NN];
-        auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, 4 independent FMA chains
-            // (one wave issues an f64 op about every 8 cycles, so 4 chains keep it busy; 8 cost 4 more adds)
-            double sa[4] = {0.0, 0.0, 0.0, 0.0};
+        auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, TGMPC_KMC independent FMA chains
+            // (capacity <= 64 without CMP; 4 elsewhere.  Round 2 chose 4 -- one wave issues an f64 op about every 8
+            // cycles -- but at two waves per SIMD the 10-deep chains' latency shows: 8 chains and 4 more adds measured
+            // +0.7 % in round 5)
+            constexpr int KC = (NN <= 64 && !CMP) ? TGMPC_KMC : 4;
+            static_assert(KC == 4 || KC == 8, "TGMPC_KMC: 4 or 8 chains");
+            double sa[KC];
+#pragma unroll
+            for (int i = 0; i < KC; ++i) sa[i] = 0.0;
             const double* vbuf = (slot >= 0) ? bcast_at(v, slot) : bcast(v);
             if constexpr (NN <= 64 && !CMP) {
                 double vb[NN];
                 lds_load_all<NN>(vbuf, vb);
 #pragma unroll
-                for (int j = 0; j < NN; ++j) sa[j & 3] = fma(Krow[j], vb[j], sa[j & 3]);
+                for (int j = 0; j < NN; ++j) sa[j % KC] = fma(Krow[j], vb[j], sa[j % KC]);
             } else {
                 // NN = 80: the whole vector in flight (160 VGPRs beside the 160 of Krow) spills inside the
                 // ADMM loop; CMP: the 3-wave budget (168) holds the row and a chunk.  CH values at a time
@@ -1115,7 +1125,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     __builtin_amdgcn_sched_group_barrier(0x002, CH, 0);
                 }
             }
-            double r = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+            double r;
+            if constexpr (KC == 8) r = ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7]));
+            else r = (sa[0] + sa[1]) + (sa[2] + sa[3]);
             // (opaque: keeps the compiler from turning the select into a branch around the whole mat-vec)
             asm volatile("" : "+v"(r));
             return own ? r : 0.0;
