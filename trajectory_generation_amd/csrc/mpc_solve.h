@@ -81,8 +81,8 @@
 #define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
 #endif
 #ifndef TGMPC_KMC
-#define TGMPC_KMC 8            // independent FMA chains of the ADMM mat-vec (K^-1 v): 4 or 8 (8: +0.7 % at the
-                               // driver's command in 3 interleaved pairs, round 5; the chains are latency-bound)
+#define TGMPC_KMC 4            // independent FMA chains of the ADMM mat-vec (K^-1 v) at capacity <= 64: 4 or 8 (8 in
+                               // the fused instance measured 9.2-9.5 M vs 13.0-13.5 M steps/s at the driver's command)
 #endif
 #ifndef TGMPC_KCH80
 #define TGMPC_KCH80 16         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec
@@ -1079,10 +1079,9 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         };
         double Krow[NN];
         auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, TGMPC_KMC independent FMA chains
-            // (capacity <= 64 without CMP; 4 elsewhere.  Round 2 chose 4 -- one wave issues an f64 op about every 8
-            // cycles -- but at two waves per SIMD the 10-deep chains' latency shows: 8 chains and 4 more adds measured
-            // +0.7 % in round 5)
-            constexpr int KC = (NN <= 64 && !CMP) ? TGMPC_KMC : 4;
+            // (capacity <= 64; 4 at capacity 80.  Round 2 chose 4 -- one wave issues an f64 op about every 8
+            // cycles; 8 chains measured far slower in the fused instance -- TGMPC_KMC)
+            constexpr int KC = NN <= 64 ? TGMPC_KMC : 4;
             static_assert(KC == 4 || KC == 8, "TGMPC_KMC: 4 or 8 chains");
             double sa[KC];
 #pragma unroll
@@ -1110,8 +1109,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                     for (int i = 0; i < CH / 2; ++i) if (c0 + CH < NN) vn[i] = v2[(c0 + CH) / 2 + i];
 #pragma unroll
                     for (int i = 0; i < CH / 2; ++i) {
-                        sa[(c0 + 2 * i) & 3] = fma(Krow[c0 + 2 * i], vb[i].x, sa[(c0 + 2 * i) & 3]);
-                        sa[(c0 + 2 * i + 1) & 3] = fma(Krow[c0 + 2 * i + 1], vb[i].y, sa[(c0 + 2 * i + 1) & 3]);
+                        sa[(c0 + 2 * i) % KC] = fma(Krow[c0 + 2 * i], vb[i].x, sa[(c0 + 2 * i) % KC]);
+                        sa[(c0 + 2 * i + 1) % KC] = fma(Krow[c0 + 2 * i + 1], vb[i].y, sa[(c0 + 2 * i + 1) % KC]);
                     }
 #pragma unroll
                     for (int i = 0; i < CH / 2; ++i) vb[i] = vn[i];
