@@ -252,16 +252,32 @@ __global__ void knet_pack_kernel(const float* __restrict__ W, int N, int K, floa
 // workgroup (thread t: output / hidden unit t & 127, K quarter t >> 7) and the quarters' partial sums
 // are added through LDS in quarter order; weight loads run KD float4 rows ahead of the FMAs, and the
 // two waves of each SIMD cover each other's L2 latency.
-constexpr int KD = 4;
+constexpr int KD = 4;   // (8 rows in flight for the GRU cells' 8-row quarters measured 71 vs 63 us per step, round 5)
+#ifndef TRAJ_KNET_PK
+#define TRAJ_KNET_PK 1   // dot_ks on explicit sequence-pair v_pk_fma_f32 (0: scalar fmaf chains, the compiler pairs them)
+#endif
 
 // acc[g][s] += sum_{k4 in [k4b, k4e)} xT[4 k4 + c][s] * P[k4][j + g * KH][c]  (P rows: NR per k4).
 // Measured on MI355X (front launch, B = 1024): this compact runtime loop 24.7 us; the same loop with
 // compile-time trip counts 27.5 us; fully unrolled straight-line code 29.4 us (register spills); a
 // cross-layer chained prefetch gave nothing -- the chain is bound by per-layer barrier / LDS / load
 // latency, not by one stalled group.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
 template <int G>
 __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const float4* __restrict__ P, int NR, int j,
                                        float (&acc)[G][KS]) {
+#if TRAJ_KNET_PK
+    // sequence pairs as packed f32 operands: v_pk_fma_f32 with the weight broadcast to both halves, the pairs straight
+    // from the LDS float4s and the accumulators -- no register moves to assemble operand pairs (the same fmaf per
+    // accumulator in the same k order as below, bit for bit)
+    f2v a2[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        a2[g][0] = f2v{acc[g][0], acc[g][1]};
+        a2[g][1] = f2v{acc[g][2], acc[g][3]};
+    }
+#endif
     float4 wb[KD][G];
 #pragma unroll
     for (int d = 0; d < KD; ++d)
@@ -281,13 +297,33 @@ __device__ __forceinline__ void dot_ks(const float* xT, int k4b, int k4e, const 
             for (int g = 0; g < G; ++g) wb[d][g] = P[(size_t)kn * NR + j + g * KH];
 #pragma unroll
             for (int g = 0; g < G; ++g) {
+#if TRAJ_KNET_PK
+                const f2v xs[4][2] = {{f2v{x0.x, x0.y}, f2v{x0.z, x0.w}}, {f2v{x1.x, x1.y}, f2v{x1.z, x1.w}},
+                                      {f2v{x2.x, x2.y}, f2v{x2.z, x2.w}}, {f2v{x3.x, x3.y}, f2v{x3.z, x3.w}}};
+                const float wc[4] = {w[g].x, w[g].y, w[g].z, w[g].w};
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+                        a2[g][h] = __builtin_elementwise_fma(xs[c][h], f2v{wc[c], wc[c]}, a2[g][h]);
+#else
                 acc[g][0] = fmaf(x3.x, w[g].w, fmaf(x2.x, w[g].z, fmaf(x1.x, w[g].y, fmaf(x0.x, w[g].x, acc[g][0]))));
                 acc[g][1] = fmaf(x3.y, w[g].w, fmaf(x2.y, w[g].z, fmaf(x1.y, w[g].y, fmaf(x0.y, w[g].x, acc[g][1]))));
                 acc[g][2] = fmaf(x3.z, w[g].w, fmaf(x2.z, w[g].z, fmaf(x1.z, w[g].y, fmaf(x0.z, w[g].x, acc[g][2]))));
                 acc[g][3] = fmaf(x3.w, w[g].w, fmaf(x2.w, w[g].z, fmaf(x1.w, w[g].y, fmaf(x0.w, w[g].x, acc[g][3]))));
+#endif
             }
         }
     }
+#if TRAJ_KNET_PK
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        acc[g][0] = a2[g][0].x;
+        acc[g][1] = a2[g][0].y;
+        acc[g][2] = a2[g][1].x;
+        acc[g][3] = a2[g][1].y;
+    }
+#endif
 }
 
 constexpr int K4_H = KH / 4;   // rows of 4 of every W_hh
