@@ -94,6 +94,8 @@ def lib():
         L.orc_mpc_step.restype = C.c_int
         L.orc_mpc_step_batch.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), C.c_int, _D, _D, _D, _D, _D,
                                          _I, _D, _D, _D, _I, _I, C.c_int]
+        L.orc_mpc_step_batch_warm.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), C.c_int, _D, _D, _D, _D, _D,
+                                              _I, _D, _I, _I, _I, C.c_int]
         L.orc_qp_exact.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), _D, _D, _D, _D, _D, _D]
         L.orc_qp_exact.restype = C.c_int
         L.orc_qp_ipm.argtypes = [C.POINTER(OrcCfg), _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, C.POINTER(OrcInfo)]
@@ -238,6 +240,27 @@ def mpc_step_batch(x0, u_prev, path_ref, vref, c: OrcCfg, p=None, nthreads=0):
     lib().orc_mpc_step_batch(C.byref(p), C.byref(c), B, _dp(x0), _dp(u_prev), _dp(path_ref), _dp(vref),
                              _dp(out["u_cmd"]), _ip(out["status"]), _dp(out["objective"]), _dp(out["X_opt"]),
                              _dp(out["U_opt"]), _ip(out["iters"]), _ip(out["polished"]), int(nthreads))
+    return out
+
+
+def mpc_step_batch_warm(x0, u_prev, path_ref, vref, rho, valid, c: OrcCfg, p=None, nthreads=0):
+    """mpc_step_batch with each instance's warm start (traj_oracle.c orc_mpc_step_batch_warm): rho [B] and valid [B]
+    are the rho carried from the instance's previous step; returns the outputs with the updated rho / valid."""
+    p = p or params()
+    N = c.N
+    x0 = _f64(x0)
+    B = x0.shape[0]
+    u_prev = _f64(u_prev, (B, 2))
+    path_ref = _f64(path_ref, (B, N + 1, 3))
+    vref = _f64(vref, (B, N + 1))
+    rho = np.ascontiguousarray(rho, dtype=np.float64).copy()
+    valid = np.ascontiguousarray(valid, dtype=np.int32).copy()
+    out = dict(u_cmd=np.zeros((B, 2)), status=np.zeros(B, np.int32), iters=np.zeros(B, np.int32),
+               polished=np.zeros(B, np.int32))
+    lib().orc_mpc_step_batch_warm(C.byref(p), C.byref(c), B, _dp(x0), _dp(u_prev), _dp(path_ref), _dp(vref),
+                                  _dp(rho), _ip(valid), _dp(out["u_cmd"]), _ip(out["status"]), _ip(out["iters"]),
+                                  _ip(out["polished"]), int(nthreads))
+    out["rho"], out["valid"] = rho, valid
     return out
 
 

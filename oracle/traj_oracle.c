@@ -1081,6 +1081,30 @@ void orc_mpc_step_batch(const orc_params* p, const orc_mpc_cfg* c, int B, const 
     }
 }
 
+/* orc_mpc_step_batch with a warm start per instance (the closed loop's carried rho, MPC/main.py's loop calling
+ * mpc_6stati.py:252-256 with warm_start=True): rho[b] / valid[b] are read as the instance's orc_warm and written
+ * back after its solve. */
+void orc_mpc_step_batch_warm(const orc_params* p, const orc_mpc_cfg* c, int B, const double* x0,
+                             const double* u_prev, const double* path_ref, const double* vref, double* rho,
+                             int* valid, double* u_cmd, int* status, int* iters, int* polished, int nthreads) {
+    int N = c->N;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+    for (int b = 0; b < B; ++b) {
+        orc_info info;
+        orc_warm w = {valid[b], rho[b]};
+        int st = orc_mpc_step_warm(p, c, x0 + 6 * b, u_prev + 2 * b, path_ref + (size_t)3 * (N + 1) * b,
+                                   vref + (size_t)(N + 1) * b, u_cmd + 2 * b, NULL, NULL, &info, &w);
+        rho[b] = w.rho;
+        valid[b] = w.valid;
+        if (status) status[b] = st;
+        if (iters) iters[b] = info.iters;
+        if (polished) polished[b] = info.polished;
+    }
+}
+
 /* ------------------------------------------- exact QP (validation solver) */
 /* Dense primal-dual interior point (Mehrotra) on the condensed QP:  min 1/2 u'Pu + q'u  s.t.  l <= A u <= u,
  * as one-sided rows G u <= h.  Independent of the ADMM path; used by tests to certify it. */

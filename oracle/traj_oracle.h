@@ -133,6 +133,10 @@ void orc_mpc_step_batch(const orc_params* p, const orc_mpc_cfg* c, int B, const 
                         const double* u_prev, const double* path_ref, const double* vref, double* u_cmd,
                         int* status, double* objective, double* X_opt, double* U_opt, int* iters,
                         int* polished, int nthreads);
+/* the same with a per-instance warm start: rho[b] / valid[b] in (an orc_warm) and out (the closed loop's carried rho) */
+void orc_mpc_step_batch_warm(const orc_params* p, const orc_mpc_cfg* c, int B, const double* x0,
+                             const double* u_prev, const double* path_ref, const double* vref, double* rho,
+                             int* valid, double* u_cmd, int* status, int* iters, int* polished, int nthreads);
 
 /* Exact QP solve used to validate the ADMM restatement (dense primal active-set on the condensed QP,
  * box+rate rows only).  Returns 0 on success. U_opt (2,N) row-major. */
