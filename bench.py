@@ -451,6 +451,8 @@ class GpuOps:
         if os.environ.get("TRAJ_QUEUE_LEAD"):    # experiments: "steps,per_mille" of the fused queue's lead set
             ls, lp = (int(v) for v in os.environ["TRAJ_QUEUE_LEAD"].split(","))
             _lib.check(_lib.lib().traj_debug_queue_lead(ls, lp), "traj_debug_queue_lead")
+        if os.environ.get("TRAJ_RUN_AHEAD"):     # experiments: the fused run's run-ahead levels (traj_debug_run_ahead)
+            _lib.check(_lib.lib().traj_debug_run_ahead(int(os.environ["TRAJ_RUN_AHEAD"])), "traj_debug_run_ahead")
 
     def sync(self):
         torch.cuda.synchronize()

@@ -255,6 +255,11 @@ int traj_debug_spin_limit(int polls);
  * ADMM iterations) run `steps` steps ahead of the level front (default 1 step, 100 per mille; 0 = plain
  * level order).  Results do not depend on it.  For experiments and tests. */
 int traj_debug_queue_lead(int steps, int per_mille);
+/* Fused-run run-ahead: a workgroup that completes an instance's step takes that instance's next step itself (no
+ * hand-off, no queue draw) while the step is at most `levels` levels past the queue's draw front (default 0 =
+ * every item from the queue in its order: measured not better across workloads).  Each item is claimed once (per-instance claim counter in the
+ * workspace).  Results do not depend on it.  For experiments and tests. */
+int traj_debug_run_ahead(int levels);
 /* Fused-run kernel instance, by waves per SIMD: 0 (default) = by capacity and launch length (capacity 40: 2, or
  * 3 from 200 steps on; capacity 80: 1); 1, 2 or 3 = forced where built (capacity 40: 2 and 3; capacity 80: 2 runs
  * the lean two-wave instance, 1 and 3 the default one-wave-per-SIMD instance; other capacities: the default).

@@ -118,7 +118,7 @@ def test_default_config_matches_oracle(L, oracle_lib):
 
 def test_workspace_bytes(L):
     for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40)):
-        assert L.traj_mpc_workspace_bytes(B, N) == (B * N * 66 + 4 * B) * 8 + ((4 * (2 * B + 2) + 7) // 8) * 8
+        assert L.traj_mpc_workspace_bytes(B, N) == (B * N * 66 + 4 * B) * 8 + ((4 * (3 * B + 2) + 7) // 8) * 8
     assert L.traj_mpc_workspace_bytes(-1, 20) == 0
 
 

@@ -540,6 +540,40 @@ def test_fused_queue_lead_bit_identical(gpu, lead):
     assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"])
 
 
+@pytest.mark.parametrize("levels,grid", [(0, 0), (1, 28), (64, 0), (64, 28), (4, 12)])
+def test_fused_run_ahead_bit_identical(gpu, levels, grid):
+    """Run-ahead (traj_debug_run_ahead: a workgroup keeps its instance for the next step, claimed once through the
+    per-instance claim counter; drawers of run-ahead items draw again) moves only the schedule: two fused launches
+    (the second ranked by the first) equal the per-step launches bit for bit, with every workgroup slot or a grid
+    far smaller than B (many instances per workgroup, many skipped draws), at N = 20 and config 3's N = 40."""
+    from trajectory_generation_amd import _lib
+    from trajectory_generation_amd.workload import make_workload
+    Ts, T, B, T0 = 0.05, 16, 80, 4
+    for N, kind in ((20, "spline"), (40, "mixed")):
+        w = make_workload(B, N, Ts, kind=kind, seed=12)
+        paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+        cfg = TB.config_struct(N=N, Ts=Ts)
+        per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+        x = torch.as_tensor(w["x0"], device=gpu).clone()
+        u = torch.as_tensor(w["u0"], device=gpu).clone()
+        vr = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=gpu)
+        hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=gpu)
+        hu = torch.empty((B, T, 2), dtype=torch.float64, device=gpu)
+        hx[:, 0] = x
+        st = torch.empty((T, B), dtype=torch.int32, device=gpu)
+        it = torch.empty((T, B), dtype=torch.int32, device=gpu)
+        try:
+            _lib.check(_lib.lib().traj_debug_run_ahead(levels), "traj_debug_run_ahead")
+            _lib.check(_lib.lib().traj_debug_fused_grid(grid), "traj_debug_fused_grid")
+            TB.closed_loop_run(x, u, paths, vr, cfg, None, 0, T0, hx, hu, st[:T0], it[:T0])
+            TB.closed_loop_run(x, u, paths, vr, cfg, None, T0, T - T0, hx, hu, st[T0:], it[T0:])
+        finally:
+            _lib.lib().traj_debug_run_ahead(4)
+            _lib.lib().traj_debug_fused_grid(0)
+        assert _same(hx, per["X"]) and _same(hu, per["U"]), N
+        assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"]), N
+
+
 def test_fused_lost_handoff_is_an_error(gpu):
     """A fused-run workgroup that gives up waiting for an instance's previous step (spin bound, here one
     poll: step 1 items are drawn while step 0 still runs) makes the run an error (TRAJ_E_HANDOFF via

@@ -52,6 +52,8 @@ def main(steps=20, warm=5, B=4096, N=20, Ts=0.05, kind="spline", out=None, lead=
         TB.closed_loop_run(x, u, paths, vref, cfg, None, 0, warm, None, None, st[:warm], it[:warm])
     items = torch.zeros((steps * B, 4), dtype=torch.int64, device=dev)
     _lib.lib().traj_debug_queue_lead(*lead)
+    if os.environ.get("TL_RA"):
+        _lib.lib().traj_debug_run_ahead(int(os.environ["TL_RA"]))
     if os.environ.get("TL_WAVES"):
         _lib.lib().traj_debug_fused_waves(int(os.environ["TL_WAVES"]))
     perm_ws = TB.workspace(B, N, dev)

@@ -111,6 +111,7 @@ _SIGS = {
     "traj_debug_fused_grid": (C.c_int, [C.c_int]),
     "traj_debug_spin_limit": (C.c_int, [C.c_int]),
     "traj_debug_queue_lead": (C.c_int, [C.c_int, C.c_int]),
+    "traj_debug_run_ahead": (C.c_int, [C.c_int]),
     "traj_debug_fused_waves": (C.c_int, [C.c_int]),
     "traj_debug_step_linearize": (C.c_int, [C.c_int]),
     "traj_debug_set_item_stamps": (C.c_int, [_V]),

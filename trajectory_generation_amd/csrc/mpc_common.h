@@ -81,10 +81,13 @@ struct KArgs {
     const int* perm;         // closed loop: instance order (longest previous solve first), or null
     int nsteps;              // > 0: fused closed loop, nsteps steps per launch (status / iters [nsteps, B])
     int fused_grid;          // fused: workgroups to launch (0: the resident slots; traj_debug_fused_grid)
-    int* queue;              // fused: [0] next work item, [1] error flag, [2 + b] completed steps of b
+    int* queue;              // fused: [0] next work item, [1] error flag, [2 + b] completed steps of b,
+                             //        [2 + B + b] steps of b claimed (drawn from the queue or run ahead)
     int spin_limit;          // fused: polls of a step counter before a hand-off is declared lost
     long long* dbg_items;    // fused diagnostics: per work item q [4]: drawn, wait over, done (100 MHz), slot
     int lead_steps, lead_h;  // fused: the heaviest lead_h ranks run lead_steps steps ahead in the queue order
+    int run_ahead;           // fused: a workgroup keeps its instance for the next step while that step is at most
+                             //        run_ahead levels past the queue's draw front (0: every step from the queue)
     int wps;                 // fused: waves per SIMD of the kernel instance to launch (2, or 3 where built)
 };
 

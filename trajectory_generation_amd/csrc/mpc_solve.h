@@ -249,6 +249,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // and every slot stays busy until the queue is drained.
     bool more = true;
     int item_of_wave = 0;   // fused: the current work item (diagnostics)
+    int ra_step = 0, ra_rank = 0;   // fused: the instance (rank) this workgroup just stepped, and its next step
     for (int step = 0; more; ++step) {
     // fused: the arguments are read through a pointer the compiler cannot see through, so nothing
     // derived from them (weights, reciprocals, per-stage predicates, address offsets) is hoisted out of
@@ -263,39 +264,94 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     long long* const dbg_items = DIAG ? a.dbg_items : nullptr;
     int b = (CLOSED && a.perm) ? a.perm[blockIdx.x] : (int)blockIdx.x;
     if constexpr (FUSED) {
-        __syncthreads();
-        if (threadIdx.x == 0) s_item = atomicAdd(&a.queue[0], 1);
-        __syncthreads();
-        const int q = s_item;
-        if (q >= a.B * a.nsteps) break;
-        if (dbg_items && threadIdx.x == 0) dbg_items[4 * (size_t)q] = __builtin_amdgcn_s_memrealtime();
-        // item q -> (step, rank).  Plain order: all ranks of step 0, then of step 1, ...  With a lead
+        // item q <-> (step, rank).  Plain order: all ranks of step 0, then of step 1, ...  With a lead
         // (a.lead_steps > 0, heavy = ranks < a.lead_h, the instances with the most ADMM iterations in the
         // previous launch): the heavy instances' first lead steps come first, then level s holds the heavy
         // instances' step s + lead followed by the light instances' step s -- the long chains are not held
         // back by the level front.  Every instance's steps stay in increasing queue order, so an item only
         // ever waits for an item drawn before it: no deadlock.
-        int rank;
-        {
-            const int Bq = a.B, S = a.nsteps;
-            const int L = (a.lead_h > 0) ? min(a.lead_steps, S) : 0, H = (L > 0) ? a.lead_h : 0;
-            const int P = L * H;
+        const int Bq = a.B, S = a.nsteps;
+        const int L = (a.lead_h > 0) ? min(a.lead_steps, S) : 0, H = (L > 0) ? a.lead_h : 0;
+        const int P = L * H, full = (S - L) * Bq;
+        auto decode = [&](int q, int& st, int& rk) -> int {   // returns the queue level of q
             if (q < P) {
-                step = q / H;
-                rank = q - step * H;
-            } else {
-                const int q1 = q - P, full = (S - L) * Bq;
-                if (q1 < full) {
-                    const int lv = q1 / Bq;
-                    rank = q1 - lv * Bq;
-                    step = (rank < H) ? lv + L : lv;
-                } else {
-                    const int q2 = q1 - full, lv = (S - L) + q2 / (Bq - H);
-                    rank = H + (q2 - (lv - (S - L)) * (Bq - H));
-                    step = lv;
+                st = q / H;
+                rk = q - st * H;
+                return 0;
+            }
+            const int q1 = q - P;
+            if (q1 < full) {
+                const int lv = q1 / Bq;
+                rk = q1 - lv * Bq;
+                st = (rk < H) ? lv + L : lv;
+                return lv;
+            }
+            const int q2 = q1 - full, lv = (S - L) + q2 / (Bq - H);
+            rk = H + (q2 - (lv - (S - L)) * (Bq - H));
+            st = lv;
+            return lv;
+        };
+        auto encode = [&](int st, int rk) -> int {
+            if (rk < H) return (st < L) ? st * H + rk : P + (st - L) * Bq + rk;
+            return (st < S - L) ? P + st * Bq + rk : P + full + (st - (S - L)) * (Bq - H) + (rk - H);
+        };
+        // Run-ahead (a.run_ahead > 0): the workgroup that completed (step - 1, rank) claims the instance's next
+        // step itself while that step is at most run_ahead levels past the draw front -- an instance whose steps
+        // are cheap runs ahead of the level order, so a long chain (a solve at the iteration cap late in the
+        // launch) starts its heavy steps earlier.  Every item is claimed exactly once: a per-instance counter
+        // (queue[2 + B + b] = steps of b claimed) taken by compare-and-swap from the value `step`, by the
+        // run-ahead or by the drawer of q; a drawer whose item was run ahead draws again.  The drawer of (s, b)
+        // waits, if it must, only for the claim of (s - 1, b), whose queue item was drawn before its own.
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int* const claim = a.queue + 2 + Bq;
+            const int total = Bq * S;
+            int got = -1;
+            if (a.run_ahead > 0 && ra_step > 0 && ra_step < S) {
+                int fs, fr;
+                const int front = __hip_atomic_load(&a.queue[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int flv = (front < total) ? decode(front, fs, fr) : S;
+                const int rlv = (ra_rank < H) ? max(ra_step - L, 0) : ra_step;   // the level of (ra_step, ra_rank)
+                const int rb = a.perm ? a.perm[ra_rank] : ra_rank;
+                if (rlv <= flv + a.run_ahead && atomicCAS(&claim[rb], ra_step, ra_step + 1) == ra_step) {
+                    got = encode(ra_step, ra_rank);
+                    if (dbg_items) dbg_items[4 * (size_t)got] = __builtin_amdgcn_s_memrealtime();
                 }
             }
+            while (got < 0) {
+                const int q = atomicAdd(&a.queue[0], 1);
+                if (q >= total) { got = q; break; }
+                const long long t_draw = __builtin_amdgcn_s_memrealtime();
+                if (a.run_ahead <= 0) { got = q; }
+                int qs, qr;
+                decode(q, qs, qr);
+                const int qb = a.perm ? a.perm[qr] : qr;
+                int spins = 0;
+                for (; got < 0;) {
+                    const int cl = __hip_atomic_load(&claim[qb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (cl > qs) break;                                              // run ahead: draw again
+                    if (cl == qs) {
+                        if (atomicCAS(&claim[qb], qs, qs + 1) == qs) { got = q; break; }
+                        continue;
+                    }
+                    __builtin_amdgcn_s_sleep(1);   // (s - 1, b) drawn, its claim not yet made
+                    if (++spins > a.spin_limit) {
+                        __hip_atomic_store(&a.queue[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        got = q;
+                        break;
+                    }
+                }
+                if (got >= 0 && dbg_items) dbg_items[4 * (size_t)q] = t_draw;   // (a run-ahead item: its claimer's)
+            }
+            s_item = got;
         }
+        __syncthreads();
+        const int q = s_item;
+        if (q >= a.B * a.nsteps) break;
+        int rank;
+        decode(q, step, rank);
+        ra_step = step + 1;
+        ra_rank = rank;
         item_of_wave = q;
         b = a.perm ? a.perm[rank] : rank;
         // issue priority (s_setprio): the wave that works on a long chain gets the SIMD first -- see the

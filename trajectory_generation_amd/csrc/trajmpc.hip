@@ -283,6 +283,15 @@ static int g_fused_grid = 0;        // traj_debug_fused_grid
 static int g_fused_waves = 0;       // traj_debug_fused_waves: 0 = by launch length, 2 or 3 = forced
 static int g_spin_limit = 1 << 22;  // traj_debug_spin_limit: polls before a fused hand-off is declared lost
 static int g_lead_steps = TGMPC_LEAD_STEPS, g_lead_permille = TGMPC_LEAD_PERMILLE;   // traj_debug_queue_lead
+// fused run: a workgroup that completes an instance's step takes the instance's next step itself while that step is
+// at most this many levels past the queue's draw front (mpc_solve.h); 0 = every item from the queue in its order.
+// Off by default: at N = 20 it only adds contention (8 levels: 11.9 M vs 12.8 M); at config 3 it moves where the
+// launch's iteration-cap chains fall -- +6.6 % on the bench's workload at 8 levels, -2.4 .. +2 % on three others
+// (profiles/r05_run_ahead*.json)
+#ifndef TGMPC_RUN_AHEAD
+#define TGMPC_RUN_AHEAD 0
+#endif
+static int g_run_ahead = TGMPC_RUN_AHEAD;   // traj_debug_run_ahead
 // traj_debug_step_linearize: the step's linearization inside the solve launch.  An atomic: a test that flips it may run
 // beside other callers of the library; each traj_mpc_step_batch reads it once.
 static std::atomic<int> g_step_inlin{1};
@@ -331,6 +340,12 @@ int traj_debug_queue_lead(int steps, int per_mille) {
     if (steps < 0 || per_mille < 0 || per_mille > 1000) return TRAJ_E_ARG;
     g_lead_steps = steps;
     g_lead_permille = per_mille;
+    return TRAJ_OK;
+}
+
+int traj_debug_run_ahead(int levels) {
+    if (levels < 0) return TRAJ_E_ARG;
+    g_run_ahead = levels;
     return TRAJ_OK;
 }
 
@@ -520,10 +535,10 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
 }
 
 // A/B/g hand-off (54 N doubles), rollout record (12 N), warm-start record (4), closed-loop order
-// (1 int), fused-run step queue (counter, error flag, completed steps per instance); a multiple of 8
+// (1 int), fused-run step queue (counter, error flag, completed and claimed steps per instance); a multiple of 8
 static size_t ws_base_bytes(int B, int N) {
     return ((size_t)B * (size_t)N * 66 + (size_t)B * 4) * sizeof(double) +
-           ((((size_t)B * 2 + 2) * sizeof(int) + 7) & ~(size_t)7);
+           ((((size_t)B * 3 + 2) * sizeof(int) + 7) & ~(size_t)7);
 }
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
@@ -653,9 +668,10 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.dbg_items = g_dbg_items;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
-    // step queue: [0] next work item, [1] error flag, [2 + b] steps of instance b completed
+    // step queue: [0] next work item, [1] error flag, [2 + b] steps of instance b completed, [2 + B + b] claimed
     a.queue = (int*)(a.wsWarm + (size_t)B * 4) + B;
-    if (hipMemsetAsync(a.queue, 0, ((size_t)B + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
+    if (hipMemsetAsync(a.queue, 0, ((size_t)B * 2 + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
+    a.run_ahead = g_run_ahead;
     stamp(0, st);
     stamp(1, st);
     stamp(2, st);
