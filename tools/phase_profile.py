@@ -5,7 +5,7 @@ import numpy as np, torch
 from trajectory_generation_amd import batch as TB, _lib
 from trajectory_generation_amd.workload import make_workload
 
-def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
+def main(B=int(os.environ.get("PP_B", 4096)), N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
     dev = TB.require_gpu()
     w = make_workload(B, N, Ts, kind=kind)
     paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
@@ -38,7 +38,7 @@ def main(B=4096, N=20, Ts=0.05, warm=5, kind="spline", polish_mode=0, fused=0):
     # may keep stamps of two different items (stores from different XCDs' L2s land in either order), and s_memtime
     # counts per XCD, so such a mix gives garbage differences.  Items whose sub-phase stamps are not one monotone
     # sequence are left out as well (counted).
-    sub_idx = [1, 20, 21, 16, 17, 18, 19, 4]
+    sub_idx = [1, 20, 21, 16, 17, 18, 19, 4] if fused else [1, 16, 17, 18, 19, 4]   # (20, 21: fused linearization)
     sd = np.diff(d[:, sub_idx], axis=1)
     ok_sub = ok & (sd >= 0).all(axis=1) & (sd < 5e8).all(axis=1)
     n_mix = int((ok & ~ok_sub).sum())

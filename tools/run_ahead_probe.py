@@ -30,7 +30,8 @@ def once(w, B, N, Ts, warm, steps, dev):
     hx[:, 0] = x
     st = torch.empty((T, B), dtype=torch.int32, device=dev)
     it = torch.empty((T, B), dtype=torch.int32, device=dev)
-    TB.closed_loop_run(x, u, paths, vref, cfg, None, 0, warm, hx, hu, st[:warm], it[:warm])
+    if warm:
+        TB.closed_loop_run(x, u, paths, vref, cfg, None, 0, warm, hx, hu, st[:warm], it[:warm])
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -43,7 +44,8 @@ def once(w, B, N, Ts, warm, steps, dev):
 def main(levels):
     dev = TB.require_gpu()
     L = _lib.lib()
-    B, Ts, warm, steps = 4096, 0.05, 5, 20
+    B, Ts = 4096, 0.05
+    warm, steps = int(os.environ.get("RA_WARM", 5)), int(os.environ.get("RA_STEPS", 20))   # (240, 0: configs[3])
     out = {}
     cases = ((20, "spline"), (40, "mixed"))
     if os.environ.get("RA_N"):   # one horizon only (20: spline, 40: mixed)
