@@ -884,6 +884,37 @@ def test_config3_hard_states_vs_fixture(gpu):
     assert du <= 1e-4, du
 
 
+def test_config3_iteration_cap_steps_vs_oracle(gpu, oracle_lib):
+    """Config 3's steps at the 10,000-iteration cap (the launch's tail): the bench's own N = 40
+    mixed workload (4096 trajectories, dt = 0.05) run 25 steps by the fused closed loop with cold rho (the oracle's
+    semantics); every step that ran to the cap (up to 12, spread over the run) is re-solved from the GPU's state by
+    the oracle: the same status and the same 10,000 iterations, the u_prev fallback where the status is not optimal,
+    and u to 1e-3 where it is (an unpolished ADMM point after 10,000 iterations)."""
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B = 40, 0.05, 25, 4096
+    w = make_workload(B, N, Ts, kind="mixed")
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=0)
+    res = {k: v.cpu().numpy() for k, v in TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg).items()}
+    cap = np.argwhere(res["iters"] == MAX_ITER)            # (t, b)
+    assert len(cap) >= 3, len(cap)                          # the workload's tail items exist
+    cap = cap[np.linspace(0, len(cap) - 1, min(12, len(cap))).round().astype(int)]
+    vr = np.tile(w["vref"], (B, 1))
+    ocfg = oracle_lib.cfg(N=N, Ts=Ts)
+    for t in np.unique(cap[:, 0]):
+        bs = cap[cap[:, 0] == t, 1]
+        xt = res["X"][:, t]
+        ut = res["U"][:, t - 1] if t > 0 else np.asarray(w["u0"])
+        prt = TB.ref_window_batch(paths, xt[:, 0], vr, N, Ts).cpu().numpy()[bs]
+        ro = oracle_lib.mpc_step_batch(xt[bs], ut[bs], prt, vr[bs], ocfg)
+        gs, gu = res["status"][t, bs], res["U"][bs, t]
+        assert np.array_equal(gs, ro["status"]), (t, bs, gs, ro["status"])
+        assert np.array_equal(ro["iters"], np.full(len(bs), MAX_ITER)), (t, bs, ro["iters"])
+        ok = gs <= 1
+        assert np.array_equal(gu[~ok], ut[bs][~ok]), (t, bs)
+        assert np.abs(gu[ok] - ro["u_cmd"][ok]).max(initial=0.0) <= 1e-3, (t, bs)
+
+
 def test_divergent_dataset_trajectory_step_gate(gpu, oracle_lib):
     """configs[3]'s rare divergent trajectory (id 1854 of the bench workload leaves the
     stable regime at dt = 0.05, vx < 0 from step 9, solver errors from ~step 70 in this build's realization):
