@@ -1,0 +1,35 @@
+"""Host side of the drop-in mpc_step (no GPU): the per-call struct cache returns the struct built for the same
+arguments (exact keys: arrays by bytes) and a fresh one for any argument that differs."""
+import numpy as np
+
+from trajectory_generation_amd import batch as TB, mpc_6stati as M
+
+
+def _cfg(**kw):
+    args = dict(N=20, Ts=0.05, q_c=6.0, q_phi=0.5, q_vx=0.5, R=np.diag([0.02, 2.0]), Rd=np.diag([0.01, 5.0]),
+                u_bounds=((-1.0, 1.0), (-0.6, 0.6)), du_bounds=((-0.5, 0.5), (-0.3, 0.3)), x_lo=None, x_hi=None)
+    args.update(kw)
+    key = [args[k] for k in ("N", "Ts", "q_c", "q_phi", "q_vx", "R", "Rd", "u_bounds", "du_bounds", "x_lo", "x_hi")]
+    return M._cached_struct("cfg", lambda: TB.config_struct(**args), *key, ())
+
+
+def test_struct_cache_same_arguments_same_struct():
+    a, b = _cfg(), _cfg()
+    assert a is b
+    assert bytes(a) == bytes(TB.config_struct(N=20, Ts=0.05))
+
+
+def test_struct_cache_distinguishes_every_argument():
+    base = _cfg()
+    for kw in (dict(N=21), dict(Ts=0.02), dict(q_c=6.5), dict(R=np.diag([0.02, 2.5])), dict(Rd=np.diag([0.02, 5.0])),
+               dict(u_bounds=((-1.0, 1.0), (-0.5, 0.6))), dict(x_lo=np.full(6, -1e3)), dict(x_hi=np.full(6, 1e3))):
+        c = _cfg(**kw)
+        assert c is not base and bytes(c) != bytes(base), kw
+        assert bytes(c) == bytes(TB.config_struct(**{**dict(N=20, Ts=0.05), **kw})), kw
+
+
+def test_struct_cache_unhashable_builds_fresh():
+    built = []
+    s1 = M._cached_struct("cfg", lambda: built.append(1) or TB.config_struct(), object())
+    s2 = M._cached_struct("cfg", lambda: built.append(1) or TB.config_struct(), object())
+    assert len(built) == 2 and s1 is not s2

@@ -21,8 +21,8 @@ reference; every computation runs in the HIP kernels of libtrajmpc.so on the GPU
     (u_prev, "Solver Error: <Exception>", {})  (:257-259).
   * `solver` is accepted and ignored (the QP is solved by the HIP ADMM); `verbose` is ignored.
   * any horizon up to 256 (the reference takes any N, :125): N <= 40 runs the register-resident hot
-    kernels, 40 < N <= 256 the general condensed-QP solver (same OSQP restatement, slower; see
-    INTEGRATION.md "Horizon tiers").
+    kernels, 40 < N <= 128 the long-horizon kernel, state bounds or N > 128 the general condensed-QP
+    solver (same OSQP restatement; see INTEGRATION.md "Horizon tiers").
 The QP's optimum is unique (R > 0), so the result is the one OSQP returns when its polish
 succeeds; see DESIGN.md "Parity" for the stated tolerances.
 """
@@ -75,6 +75,16 @@ class _CallIO:
             io = cls._cache[k] = cls(dev, nin, nf, ni)
         return io
 
+    def step_ptrs(self, N: int):
+        """The step entry point's argument pointers into d_in / d_out (fixed per buffer; built once)."""
+        if getattr(self, "_ptrs", None) is None:
+            i, o, d = self.d_in.data_ptr(), self.d_out.data_ptr(), 8
+            oi = o + d * self.nf
+            self._ptrs = tuple(C.c_void_p(v) for v in (
+                i, i + d * 6, i + d * 8, i + d * (8 + 3 * (N + 1)),                       # x0, u_prev, path_ref, vref
+                o, oi, o + d * 2, o + d * 3, o + d * (3 + 6 * (N + 1)), oi + 4, oi + 8))  # u_cmd, status, obj, X, U, it, pol
+        return self._ptrs
+
     def send(self):
         self.d_in.copy_(self.h_in, non_blocking=True)
 
@@ -89,6 +99,36 @@ class _CallIO:
 
 
 _PSD_CACHE: dict = {}
+_STRUCT_CACHE: dict = {}
+
+
+def _frozen(v):
+    """A hashable, exact key for an mpc_step argument (arrays by shape and bytes), or None when there is none."""
+    if v is None or isinstance(v, (bool, int, float, str)):
+        return ("s", v)
+    if isinstance(v, np.ndarray):
+        return ("a", v.shape, v.dtype.str, v.tobytes())
+    if isinstance(v, (tuple, list)):
+        parts = tuple(_frozen(e) for e in v)
+        return None if any(e is None for e in parts) else ("t", parts)
+    if isinstance(v, np.generic):
+        return ("s", v.item())
+    return None
+
+
+def _cached_struct(kind, build, *key_parts):
+    """config_struct / params_struct for the same arguments as a previous call: the same ctypes struct (the C side
+    copies it at each launch and never writes it).  Arguments without an exact key are built afresh."""
+    parts = tuple(_frozen(k) for k in key_parts)
+    if any(k is None for k in parts):
+        return build()
+    key = (kind,) + parts
+    v = _STRUCT_CACHE.get(key)
+    if v is None:
+        if len(_STRUCT_CACHE) > 256:
+            _STRUCT_CACHE.clear()
+        v = _STRUCT_CACHE[key] = build()
+    return v
 
 
 def _is_psd_cached(M: np.ndarray) -> bool:
@@ -211,8 +251,11 @@ def mpc_step(
     if not (_is_psd_cached(R) and _is_psd_cached(Rd)):
         # cvxpy rejects a non-convex quad_form at prob.solve (inside the reference's try, :255-259)
         return u_pr, "Solver Error: DCPError", {}
-    cfg = _b.config_struct(N=N, Ts=Ts, q_c=q_c, q_phi=q_phi, q_vx=q_vx, R=R, Rd=Rd, u_bounds=u_bounds,
-                           du_bounds=du_bounds, x_lo=x_lo, x_hi=x_hi, **solver_settings)
+    cfg = _cached_struct(
+        "cfg", lambda: _b.config_struct(N=N, Ts=Ts, q_c=q_c, q_phi=q_phi, q_vx=q_vx, R=R, Rd=Rd, u_bounds=u_bounds,
+                                        du_bounds=du_bounds, x_lo=x_lo, x_hi=x_hi, **solver_settings),
+        N, Ts, q_c, q_phi, q_vx, R, Rd, u_bounds, du_bounds, x_lo, x_hi, tuple(sorted(solver_settings.items())))
+    pst = _cached_struct("params", lambda: _b.params_struct(p), tuple(sorted(p.items())))
     # one staged copy in: [x0 6 | u_prev 2 | path_ref 3(N+1) | vref N+1]; one copy out:
     # [u_cmd 2 | objective 1 | X_opt 6(N+1) | U_opt 2N | status, iters, polished (int32)]
     dev = _b.require_gpu()
@@ -224,14 +267,15 @@ def mpc_step(
     a[8:8 + 3 * (N + 1)] = np.asarray(path_ref, np.float64).reshape(-1)
     a[8 + 3 * (N + 1):] = np.asarray(vref, np.float64).reshape(-1)
     io.send()
-    d, do = io.d_in, io.d_out
-    ints = do[nf:].view(torch.int32)
-    out = {"u_cmd": do[0:2].view(1, 2), "objective": do[2:3], "X_opt": do[3:3 + 6 * (N + 1)].view(1, 6, N + 1),
-           "U_opt": do[3 + 6 * (N + 1):nf].view(1, 2, N), "status": ints[0:1], "iters": ints[1:2],
-           "polished": ints[2:3]}
+    # the step entry point on the staged buffers directly (batch.mpc_step_batch's launch for B = 1, without its
+    # per-call tensor views and conversions)
+    sb = int(_b._lib.lib().traj_mpc_sb_workspace_bytes(1, N)) if _b._general(cfg) else 0
+    ws = _b.workspace(1, N, dev, sb, role="step")
     try:
-        _b.mpc_step_batch(d[:6].view(1, 6), d[6:8].view(1, 2), d[8:8 + 3 * (N + 1)].view(1, N + 1, 3),
-                          d[8 + 3 * (N + 1):].view(1, N + 1), cfg, p, out=out)
+        _b._lib.check(_b._lib.lib().traj_mpc_step_batch(C.byref(pst), C.byref(cfg), 1, *io.step_ptrs(N),
+                                                        C.c_void_p(ws.data_ptr()), ws.numel() * 8,
+                                                        C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                      "traj_mpc_step_batch")
     except BaseException:
         io.abort()
         raise
