@@ -80,6 +80,10 @@
 #ifndef TGMPC_PMUL_W2
 #define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
 #endif
+#ifndef TGMPC_KMC80
+#define TGMPC_KMC80 4          // the same at capacity 80 (one wave per SIMD): 8 measured 0.87 M vs 0.93 M at config 3
+                               // (and with 40-value chunks 0.85 M; round 5, profiles/r05_kmc80_ab_n40.txt)
+#endif
 #ifndef TGMPC_KMC
 #define TGMPC_KMC 4            // independent FMA chains of the ADMM mat-vec (K^-1 v) at capacity <= 64: 4 or 8 (8 in
                                // the fused instance measured 9.2-9.5 M vs 13.0-13.5 M steps/s at the driver's command)
@@ -1137,7 +1141,7 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
         auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, TGMPC_KMC independent FMA chains
             // (capacity <= 64; 4 at capacity 80.  Round 2 chose 4 -- one wave issues an f64 op about every 8
             // cycles; 8 chains measured far slower in the fused instance -- TGMPC_KMC)
-            constexpr int KC = NN <= 64 ? TGMPC_KMC : 4;
+            constexpr int KC = NN <= 64 ? TGMPC_KMC : TGMPC_KMC80;
             static_assert(KC == 4 || KC == 8, "TGMPC_KMC: 4 or 8 chains");
             double sa[KC];
 #pragma unroll
