@@ -663,7 +663,10 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     // kernel instance: capacity 40, 2 waves per SIMD (3 from TRAJ_FUSED_W3_MIN_STEPS steps when that is set); capacity
     // 80, one wave per SIMD (the lean two-wave instance, traj_debug_fused_waves(2), spills at its 256 registers)
     constexpr int w3_min = TRAJ_FUSED_W3_MIN_STEPS;
-    a.wps = g_fused_waves ? g_fused_waves : (2 * c->N > 64 ? 1 : ((w3_min > 0 && steps >= w3_min) ? 3 : 2));
+    // (by the capacity launch_mpc picks: n = 2N > 40 runs capacity 80 -- 64 only in a TGMPC_CAP64 build, whose fused
+    // launch ignores wps -- so 20 < N <= 32 takes the one-wave-per-SIMD instance too; until round 5 it fell through
+    // to the opt-in lean two-wave instance, which spills: N = 30 ran 0.68 M against N = 40's 0.99 M)
+    a.wps = g_fused_waves ? g_fused_waves : (2 * c->N > 40 ? 1 : ((w3_min > 0 && steps >= w3_min) ? 3 : 2));
     a.spin_limit = g_spin_limit;
     a.dbg_items = g_dbg_items;
     carve_workspace(a, workspace, B, c->N);
