@@ -89,7 +89,9 @@
                                // the fused instance measured 9.2-9.5 M vs 13.0-13.5 M steps/s at the driver's command)
 #endif
 #ifndef TGMPC_KCH80
-#define TGMPC_KCH80 16         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec
+#define TGMPC_KCH80 40         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec (round 5,
+                               // under the max-ILP scheduler: 40 0.965-0.969 M at config 3, 16 0.952, 80 0.946, 20 0.935,
+                               // 8 0.933; profiles/r05_cap80_knobs_ab.txt)
 #endif
 #ifndef TGMPC_PCH80
 #define TGMPC_PCH80 4          // capacity 80, one wave per SIMD: pivot-row double2 per chunk of the sweep (0: whole row)
