@@ -75,7 +75,8 @@
 #define TGMPC_RECV2 1          // capacity 80, one wave per SIMD: the receiver-lane sweep (one fma per entry and pivot)
 #endif
 #ifndef TGMPC_COND80
-#define TGMPC_COND80 0         // capacity 80, one wave per SIMD: the condensing reads the F rows in chunks of 8
+#define TGMPC_COND80 1         // capacity 80, one wave per SIMD: the condensing reads the F rows in chunks of 8 (round 5,
+                               // under the max-ILP scheduler: config 3 0.967 -> 0.993 M, profiles/r05_cap80_knobs_ab.txt)
 #endif
 #ifndef TGMPC_PMUL_W2
 #define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
