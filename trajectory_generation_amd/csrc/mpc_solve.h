@@ -81,6 +81,9 @@
 #ifndef TGMPC_PMUL_W2
 #define TGMPC_PMUL_W2 0        // one-wave fused instances at 2 waves per SIMD: the rolled P v as well
 #endif
+#ifndef TGMPC_RESMAX2
+#define TGMPC_RESMAX2 1        // two-wave residual checks: the maxima by an LDS-transposed reduction (0: block_max)
+#endif
 #ifndef TGMPC_KMC80
 #define TGMPC_KMC80 4          // the same at capacity 80 (one wave per SIMD): 8 measured 0.87 M vs 0.93 M at config 3
                                // (and with 40-value chunks 0.85 M; round 5, profiles/r05_kmc80_ab_n40.txt)
@@ -1252,6 +1255,36 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
                 lds_load_all<8>(s_F, mv);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) v[i] = nan[i] ? __builtin_nan("") : mv[i];
+                __syncthreads();
+            } else if constexpr (TGMPC_RESMAX2 && WAVES == 2 && !LEAN) {
+                // two waves: the same transposed reduction over the exchange buffers (free here: every product of
+                // this check is in registers once the first barrier is passed) -- 8 values x NN rows, lane 8 i + p
+                // of wave 0 takes rows [p NN/8, (p+1) NN/8) of value i, three DPP steps, 8 maxima back; block_max's
+                // 6 x 8 cross-lane shuffles per wave are gone.  A NaN-propagating max (the values are >= +0, so the
+                // order of the maxima does not matter, bit for bit)
+                static_assert(NN % 8 == 0 && 8 * NN + 8 <= NEX, "s_ex too small");
+                constexpr int PL = NN / 8;
+                auto nmax = [](double a_, double b_) { return (a_ > b_ || a_ != a_) ? a_ : b_; };
+                double* const tb = s_ex;
+                __syncthreads();
+                if (t < NN) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) tb[i * NN + t] = v[i];
+                }
+                __syncthreads();
+                if (t < 64) {
+                    const double* src = tb + (t >> 3) * NN + (t & 7) * PL;
+                    double m = src[0];
+#pragma unroll
+                    for (int k = 1; k < PL; ++k) m = nmax(m, src[k]);
+                    m = nmax(m, dpp_d<0xB1>(m));    // lane ^ 1
+                    m = nmax(m, dpp_d<0x4E>(m));    // lane ^ 2
+                    m = nmax(m, dpp_d<0x141>(m));   // half-row mirror: quads of one 8-lane group
+                    if ((t & 7) == 0) tb[8 * NN + (t >> 3)] = m;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < 8; ++i) v[i] = tb[8 * NN + i];
                 __syncthreads();
             } else {
                 block_max(v);
