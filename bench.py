@@ -614,6 +614,15 @@ def parse_args(argv=None):
                     help="directory: rank 0 also writes the dataset CSVs there (timed separately)")
     ap.add_argument("--no-cold", action="store_true",
                     help="skip the reference-semantics (cold-start) pass reported as 'cold'")
+    ap.add_argument("--no-config3", dest="config3", action="store_false",
+                    help="skip the configs[2] object (N = 40, mixed references, same steps / warmup; one GPU)")
+    ap.add_argument("--config3-traffic-json", default=os.path.join(HERE, "profiles", "traffic_r05_n40.json"))
+    ap.add_argument("--config3-issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r05_n40.json"))
+    ap.add_argument("--config3-stall-json", default=os.path.join(HERE, "profiles", "r06_pmc_stall_n40.json"))
+    ap.add_argument("--config3-cpu-traj", type=int, default=512)
+    ap.add_argument("--config3-cpu-steps", type=int, default=16)
+    ap.add_argument("--no-host-io", dest="host_io", action="store_false",
+                    help="skip the end-to-end (H2D + run + D2H) variant of the headline ('host_io')")
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds before a process-group rendezvous or collective gives up (N > 1)")
     args = ap.parse_args(argv)
@@ -682,11 +691,38 @@ def _main_ranked(args, ops_factory, backend, world_env, rank, local):
     return out
 
 
-def bench_run(args, ops, dist, rank, world):
-    """One rank's bench: warmup, the timed region bracketed by barrier + synchronize on both sides, the
-    max-over-ranks elapsed time, the dataset leg; rank 0 returns the JSON record (None elsewhere)."""
-    N, Ts, B = args.horizon, args.dt, args.batch
-    w = make_workload(B, N, Ts, kind=args.kind, seed=0, id_offset=rank * B)
+def _load_profile(path, **want):
+    """A profile JSON (tools/pmc_*.py output) if it describes this launch, else None -- and why, so that a line whose
+    roofline.traffic / roofline.issue is null says which file was looked at and what did not match."""
+    if not path or not os.path.exists(path):
+        return None, f"{os.path.relpath(os.path.abspath(path), HERE) if path else path}: not found"
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError) as e:
+        return None, f"{os.path.relpath(path, HERE)}: unreadable ({e})"
+    for k, v in want.items():
+        have = d.get(k, 20 if k == "horizon" else None)
+        if k == "fused":
+            have = bool(d.get("fused", False))
+        if have != v:
+            return None, f"{os.path.relpath(path, HERE)}: {k} = {have}, this launch has {v}"
+    return d, None
+
+
+def f64_flop_algorithmic(N, K):
+    """F(N, K) = N (60 + 150) + 72 N (N + 1) + (N + 1)(72 N + 24 N^2) + 8 N^3 / 3 + K (8 N^2 + 20 N)
+    algorithmic f64 FLOP per MPC step, K = mean ADMM iterations."""
+    return N * 210 + 72 * N * (N + 1) + (N + 1) * (72 * N + 24 * N * N) + 8 * N ** 3 / 3 + K * (8 * N * N + 20 * N)
+
+
+def mpc_leg(args, ops, dist, rank, world, N, kind, traffic_json, issue_json, stall_json=None, with_cold=True):
+    """One closed-loop MPC measurement: --warmup untimed steps, then EXACTLY --steps timed steps bracketed by barrier +
+    synchronize on both sides (max over ranks), state resident in HBM; the roofline object of the dominant kernel
+    (solve_kernel, HIP events on its launch stream), the PMC traffic / issue profiles if they describe this launch,
+    and (with_cold) the same command with cold rho.  Returns (record, state, workload, iterations, statuses)."""
+    Ts, B = args.dt, args.batch
+    w = make_workload(B, N, Ts, kind=kind, seed=0, id_offset=rank * B)
     T = args.warmup + args.steps
     fused = not args.per_step
 
@@ -720,8 +756,8 @@ def bench_run(args, ops, dist, rank, world):
     # per call makes its warm_start=True a no-op (mpc_6stati.py:252-256) -- reported beside it ("cold").
     s, elapsed = timed_pass(1, True)
     kernels_ms = ops.kernel_times()
-    s_cold = cold = None
-    if not args.no_cold:
+    cold = None
+    if with_cold:
         s_cold, el_cold = timed_pass(0, False)
         ic = s_cold["it"][args.warmup:].cpu().numpy().reshape(-1)
         cold = {"what": "the same command with warm_start=0 (cold rho every step, the reference's effective "
@@ -735,82 +771,144 @@ def bench_run(args, ops, dist, rank, world):
     steps_per_launch = args.steps if fused else 1
     iters = s["it"][args.warmup:].cpu().numpy().reshape(-1)
     stat = s["st"][args.warmup:].cpu().numpy().reshape(-1)
-    dataset = dataset_leg(args, w, ops, dist, rank, world) if args.dataset_steps > 0 else None
-    if rank != 0:
-        return None
-
-    total = world * B * args.steps
-    value = total / elapsed
+    value = world * B * args.steps / elapsed
     kmax = s["kmax"]
     bytes_launch = B * algorithmic_bytes_per_traj(N, kmax) * steps_per_launch
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
     traffic = traffic_step = None
-    if os.path.exists(args.traffic_json):
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("horizon") == N and bool(tj.get("fused", False)) == fused:
-                if fused and tj.get("hbm_bytes_per_instance_step"):
-                    # PMC bytes per instance-step of the profiled fused launch x this launch's instance-steps
-                    traffic = float(tj["hbm_bytes_per_instance_step"]) * B * steps_per_launch
-                    traffic_step = float(tj["hbm_bytes_per_instance_step"]) * B
-                elif tj.get("batch") == B and int(tj.get("steps_per_launch", 1)) == steps_per_launch:
-                    traffic = tj.get("hbm_bytes_per_kernel", {}).get("solve_kernel")
-                    traffic_step = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
-            traffic = traffic_step = None
+    tj, traffic_why = _load_profile(traffic_json, horizon=N, fused=fused)
+    if tj is not None:
+        if fused and tj.get("hbm_bytes_per_instance_step"):
+            # PMC bytes per instance-step of the profiled fused launch x this launch's instance-steps
+            traffic = float(tj["hbm_bytes_per_instance_step"]) * B * steps_per_launch
+            traffic_step = float(tj["hbm_bytes_per_instance_step"]) * B
+        elif tj.get("batch") == B and int(tj.get("steps_per_launch", 1)) == steps_per_launch:
+            traffic = tj.get("hbm_bytes_per_kernel", {}).get("solve_kernel")
+            traffic_step = tj.get("hbm_bytes_per_launch")
+        else:
+            traffic_why = f"{os.path.relpath(traffic_json, HERE)}: batch / steps_per_launch differ from this launch"
     issue = None
-    if os.path.exists(args.issue_json):
+    ij, issue_why = _load_profile(issue_json, batch=B, horizon=N)
+    if ij is not None:
         try:
-            with open(args.issue_json) as f:
-                ij = json.load(f)
-            if ij.get("batch") == B and ij.get("horizon", 20) == N:
-                # solve_kernel is VALU-issue/latency bound: the issued f64 lane-FLOP rate against the f64
-                # vector peak, and the VALU issue slots used (4 cycles per wave64 instruction)
-                fl = ij["f64_flop_issued_per_step"] * value / world / 1e12
-                # F(N, K) = N (60 + 150) + 72 N (N + 1) + (N + 1)(72 N + 24 N^2) + 8 N^3 / 3
-                #                 + K (8 N^2 + 20 N) algorithmic f64 FLOP per step, K = mean ADMM iterations
-                K = float(iters.mean())
-                f_alg = (N * 210 + 72 * N * (N + 1) + (N + 1) * (72 * N + 24 * N * N) + 8 * N ** 3 / 3
-                         + K * (8 * N * N + 20 * N))
-                fa = f_alg * value / world / 1e12
-                issue = {"what": "solve_kernel issue side (PMC SQ_INSTS_VALU*, per instance-step x steps/s)",
-                         "f64_tflops_issued": fl, "f64_peak_tflops": F64_VECTOR_PEAK_TF,
-                         "f64_frac": fl / F64_VECTOR_PEAK_TF,
-                         "f64_flop_algorithmic_per_step": f_alg, "f64_tflops_algorithmic": fa,
-                         "f64_frac_algorithmic": fa / F64_VECTOR_PEAK_TF,
-                         "valu_insts_per_step": ij["valu_insts_per_step"],
-                         "valu_issue_frac": ij["valu_insts_per_step"] * 4 * value / world / (SIMDS * CLOCK_HZ),
-                         "source": os.path.relpath(args.issue_json, HERE)}
-                if "f64_valu_insts_per_step" in ij:
-                    # SIMD VALU busy time on CDNA4 (MI355X_MICROARCH.md, per-instruction constants): a wave64
-                    # f64 instruction holds the 16-lane f64 pipe 4 cycles, any other VALU instruction the
-                    # 32-wide SIMD 2 cycles
-                    f64i = ij["f64_valu_insts_per_step"]
-                    issue["simd_valu_busy_frac"] = ((f64i * 4 + (ij["valu_insts_per_step"] - f64i) * 2) * value / world
-                                                    / (SIMDS * CLOCK_HZ))
-        except (OSError, ValueError, KeyError):
-            issue = None
-    if issue is not None and fused and N == 20 and B == 4096 and os.path.exists(args.stall_json):   # (the profiled config)
-        try:
-            with open(args.stall_json) as f:
-                sc = json.load(f)["counters"]
-            # measured SIMD VALU occupancy of the profiled 20-step launch: SQ_ACTIVE_INST_VALU (quad-cycles, summed
-            # over waves) x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) -- no clock assumption (MI355X_MICROARCH.md)
-            issue["simd_valu_active_frac_pmc"] = sc["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * sc["GRBM_GUI_ACTIVE"] / 8.0)
-            issue["wave_cycle_split_pmc"] = {k: sc[k] / sc["SQ_WAVE_CYCLES"] for k in
-                                             ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")}
-            issue["stall_source"] = os.path.relpath(args.stall_json, HERE)
-        except (OSError, ValueError, KeyError, ZeroDivisionError):
-            pass
+            # solve_kernel is VALU-issue/latency bound: the issued f64 lane-FLOP rate against the f64
+            # vector peak, and the VALU issue slots used (4 cycles per wave64 instruction)
+            fl = ij["f64_flop_issued_per_step"] * value / world / 1e12
+            K = float(iters.mean())
+            f_alg = f64_flop_algorithmic(N, K)
+            fa = f_alg * value / world / 1e12
+            issue = {"what": "solve_kernel issue side (PMC SQ_INSTS_VALU*, per instance-step x steps/s)",
+                     "f64_tflops_issued": fl, "f64_peak_tflops": F64_VECTOR_PEAK_TF,
+                     "f64_frac": fl / F64_VECTOR_PEAK_TF,
+                     "f64_flop_algorithmic_per_step": f_alg, "f64_tflops_algorithmic": fa,
+                     "f64_frac_algorithmic": fa / F64_VECTOR_PEAK_TF,
+                     "issued_over_algorithmic": ij["f64_flop_issued_per_step"] / f_alg,
+                     "valu_insts_per_step": ij["valu_insts_per_step"],
+                     "valu_issue_frac": ij["valu_insts_per_step"] * 4 * value / world / (SIMDS * CLOCK_HZ),
+                     "source": os.path.relpath(issue_json, HERE)}
+            if "f64_valu_insts_per_step" in ij:
+                # SIMD VALU busy time on CDNA4 (MI355X_MICROARCH.md, per-instruction constants): a wave64
+                # f64 instruction holds the 16-lane f64 pipe 4 cycles, any other VALU instruction the
+                # 32-wide SIMD 2 cycles
+                f64i = ij["f64_valu_insts_per_step"]
+                issue["simd_valu_busy_frac"] = ((f64i * 4 + (ij["valu_insts_per_step"] - f64i) * 2) * value / world
+                                                / (SIMDS * CLOCK_HZ))
+        except (KeyError, TypeError, ZeroDivisionError) as e:
+            issue, issue_why = None, f"{os.path.relpath(issue_json, HERE)}: missing field ({e})"
+    if issue is not None and fused and stall_json:
+        sj, stall_why = _load_profile(stall_json)
+        if sj is not None and sj.get("batch", B) == B and sj.get("horizon", 20) == N:
+            try:
+                sc = sj["counters"]
+                # measured SIMD VALU occupancy of the profiled launch: SQ_ACTIVE_INST_VALU (quad-cycles, summed over
+                # waves) x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) -- no clock assumption (MI355X_MICROARCH.md)
+                issue["simd_valu_active_frac_pmc"] = sc["SQ_ACTIVE_INST_VALU"] * 4.0 / (SIMDS * sc["GRBM_GUI_ACTIVE"] / 8.0)
+                issue["wave_cycle_split_pmc"] = {k: sc[k] / sc["SQ_WAVE_CYCLES"] for k in
+                                                 ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY")}
+                issue["stall_source"] = os.path.relpath(stall_json, HERE)
+            except (KeyError, ZeroDivisionError):
+                pass
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
+            "kernel": f"solve_kernel<{_capacity(2 * N)},true>" + (
+                f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
+            "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
+            "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,
+            "traffic_source": os.path.relpath(os.path.abspath(traffic_json), HERE) if traffic is not None else None,
+            "issue": issue}
+    if traffic is None:
+        roof["traffic_rejected"] = traffic_why
+    if issue is None:
+        roof["issue_rejected"] = issue_why
+    rec = {"value": value, "ms_per_step": 1e3 * elapsed / args.steps, "roofline": roof,
+           "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
+                            "iters_max": int(iters.max()), "status_hist": np.bincount(stat, minlength=7).tolist()},
+           "cold": cold}
+    return rec, s, w
+
+
+def host_io_measure(args, ops, w, N, reps=3):
+    """SURVEY.md 8(d)'s end-to-end variant of the headline (kernel + H2D/D2H inside the timed region): the host hands
+    over x0, u_prev, the reference paths and vref in pageable numpy arrays, the W + K closed-loop steps run (the same
+    fused launches as the headline), and the histories X [B,T+1,6], U [B,T,2], status / iters [T,B] come back to
+    host numpy.  Median of `reps` runs; the headline's `value` keeps the inputs resident in HBM (the task's contract)."""
+    B, Ts = args.batch, args.dt
+    T = args.warmup + args.steps
+    fused = not args.per_step
+    times = []
+    for _ in range(reps + 1):
+        ops.sync()
+        t0 = time.perf_counter()
+        s = ops.setup(w, B, N, Ts, T, args.polish_mode, warm_start=1)       # H2D: states, paths, vref
+        if args.warmup:
+            ops.run(s, 0, args.warmup, fused)
+        ops.run(s, args.warmup, args.steps, fused)
+        out = [s[k].cpu().numpy() for k in ("hx", "hu", "st", "it")]      # D2H: the histories
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times[1:]))
+    h2d = sum(int(np.asarray(w[k]).nbytes) for k in ("x0", "u0")) + B * (N + 1) * 8
+    d2h = sum(int(a.nbytes) for a in out)
+    return {"what": "end to end from host arrays: upload x0 / u_prev / paths / vref, W + K closed-loop steps (fused), "
+                    "download X / U / status / iters histories (SURVEY.md 8(d) 'kernel + H2D/D2H inside the timed region')",
+            "value": B * T / dt, "unit": "MPC steps/s", "steps": T, "seconds": dt, "d2h_bytes": d2h,
+            "h2d_bytes_min": h2d, "reps": reps}
+
+
+def bench_run(args, ops, dist, rank, world):
+    """One rank's bench: warmup, the timed region bracketed by barrier + synchronize on both sides, the
+    max-over-ranks elapsed time, the dataset leg; rank 0 returns the JSON record (None elsewhere)."""
+    N, Ts, B = args.horizon, args.dt, args.batch
+    fused = not args.per_step
+    stall = args.stall_json if (N == 20 and B == 4096) else None    # (the profiled config)
+    rec, s, w = mpc_leg(args, ops, dist, rank, world, N, args.kind, args.traffic_json, args.issue_json, stall,
+                        with_cold=not args.no_cold)
+    dataset = dataset_leg(args, w, ops, dist, rank, world) if args.dataset_steps > 0 else None
+    # config 3 (BASELINE.json configs[2]): 4096 mixed sinusoid / parabola references, N = 40, same K / W -- its own line
+    # object beside the headline, measured by the same timed region (one GPU)
+    cfg3 = None
+    if args.config3 and world == 1 and not (N == 40 and args.kind == "mixed"):
+        r3, _, w3 = mpc_leg(args, ops, dist, rank, world, 40, "mixed", args.config3_traffic_json,
+                            args.config3_issue_json, args.config3_stall_json, with_cold=False)
+        cfg3 = dict({"metric": f"MPC steps/sec (batch={B}, N=40, mixed sinusoid/parabola references)",
+                     "unit": "MPC steps/s", "steps": args.steps, "warmup": args.warmup,
+                     "config": {"workload": f"closed-loop mixed (50 % sinusoid, 50 % parabola) tracking MPC, {B} "
+                                            f"trajectories, N=40, dt={Ts}s (BASELINE.json configs[2])",
+                                "horizon": 40, "dt": Ts, "batch": B}}, **r3)
+        if not args.no_cpu:
+            cfg3["cpu_baseline"] = cpu_baseline(w3, 40, Ts, min(args.config3_cpu_traj, B), args.config3_cpu_steps,
+                                                args.polish_mode, 1)
+    host_io = host_io_measure(args, ops, w, N) if (args.host_io and world == 1 and fused) else None
+    if rank != 0:
+        return None
+
     out = {
         "metric": "MPC steps/sec (batch=4096, N=20)" if (B == 4096 and N == 20) else f"MPC steps/sec (batch={B}, N={N})",
-        "value": value,
+        "value": rec["value"],
         "unit": "MPC steps/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
+        "ms_per_step": rec["ms_per_step"],
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -820,21 +918,17 @@ def bench_run(args, ops, dist, rank, world):
                    "global_batch": world * B, "horizon": N, "dt": Ts, "parallelism": f"shard{world}",
                    "solver": f"ADMM(OSQP restated)+polish mode {args.polish_mode}, fp64",
                    "warm_start": "rho carried from the instance's previous step (closed loop); cold: see 'cold'",
-                   "launch": "fused traj_closed_loop_run" if fused else "traj_closed_loop_step per step"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
-                     "kernel": f"solve_kernel<{_capacity(2 * N)},true>" + (
-                         f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
-                     "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
-                     "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,
-                     "traffic_source": os.path.relpath(os.path.abspath(args.traffic_json), HERE) if traffic is not None else None,
-                     "issue": issue},
-        "solver_stats": {"iters_mean": float(iters.mean()), "iters_p99": float(np.percentile(iters, 99)),
-                         "iters_max": int(iters.max()),
-                         "status_hist": np.bincount(stat, minlength=7).tolist()},
+                   "launch": "fused traj_closed_loop_run" if fused else "traj_closed_loop_step per step",
+                   "timed_region": "device-resident state: x0 / u_prev / paths / vref uploaded and histories left in "
+                                   "HBM outside the timed region (H2D / D2H excluded); the end-to-end variant with both "
+                                   "inside is 'host_io'"},
+        "roofline": rec["roofline"],
+        "solver_stats": rec["solver_stats"],
     }
-    out["cold"] = cold
+    out["cold"] = rec["cold"]
     out["dataset"] = dataset
+    out["host_io"] = host_io
+    out["config3"] = cfg3
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(w, N, Ts, min(args.cpu_traj, B), args.cpu_steps, args.polish_mode,
                                            s["cfg"].warm_start)

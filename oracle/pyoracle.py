@@ -110,8 +110,39 @@ def lib():
                                       C.c_int, _D, _D, _I, _I]
         L.orc_closed_loop_batch.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcCfg), C.POINTER(OrcPath), C.c_int,
                                             _D, _D, _D, C.c_int, _D, _D, _I, _I, C.c_int]
+        L.orc_set_tire_sine.argtypes = [C.c_int]
+        L.orc_set_tire_sine.restype = C.c_int
+        L.orc_tire_sin.argtypes = [C.c_double]
+        L.orc_tire_sin.restype = C.c_double
         _lib = L
     return _lib
+
+
+def set_tire_sine(mode: int) -> int:
+    """0: libm sin in the tire forces (default, pinned by the reference fixtures); 1: the HIP path's bounded-range
+    polynomial (physics.h tire_sin_poly, same coefficients and fma order).  Returns the previous mode."""
+    return int(lib().orc_set_tire_sine(int(mode)))
+
+
+def tire_sin(z) -> np.ndarray:
+    """The oracle's tire sine in the current mode, elementwise."""
+    f = lib().orc_tire_sin
+    return np.array([f(float(v)) for v in np.asarray(z, np.float64).reshape(-1)]).reshape(np.shape(z))
+
+
+class tire_sine:
+    """Context manager: `with tire_sine(1): ...` runs the oracle with the HIP path's tire sine, then restores."""
+
+    def __init__(self, mode: int):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = set_tire_sine(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_tire_sine(self.prev)
+        return False
 
 
 def _dp(a):

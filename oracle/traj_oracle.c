@@ -71,6 +71,38 @@ static double np_sign(double x) {
     return x;
 }
 
+/* The tire sine sin(C atan(B alpha)) (mpc_6stati.py:46-47).  Mode 0 (default): libm's sin, what the reference
+ * fixtures pin.  Mode 1: the GPU's bounded-range polynomial, restated coefficient for coefficient and in the same
+ * Horner/fma order as trajmpc's physics.h tire_sin_poly (odd Taylor polynomial through x^21 on |z| <= pi/2, libm's
+ * sin outside), so that the oracle and the HIP path evaluate the same tire physics and a parity gate that compares
+ * unconverged points (the 10,000-iteration cap) tests the solver, not the sine.  Process-global; set it before a
+ * batch runs (orc_set_tire_sine). */
+static int g_tire_sine = 0;
+int orc_set_tire_sine(int mode) {
+    int prev = g_tire_sine;
+    g_tire_sine = mode ? 1 : 0;
+    return prev;
+}
+static double tire_sin_poly(double x) {
+    const double x2 = x * x;
+    double q = 1.9572941063391263e-20;
+    q = fma(q, x2, -8.22063524662433e-18);
+    q = fma(q, x2, 2.8114572543455206e-15);
+    q = fma(q, x2, -7.647163731819816e-13);
+    q = fma(q, x2, 1.6059043836821613e-10);
+    q = fma(q, x2, -2.505210838544172e-08);
+    q = fma(q, x2, 2.7557319223985893e-06);
+    q = fma(q, x2, -0.0001984126984126984);
+    q = fma(q, x2, 0.008333333333333333);
+    q = fma(q, x2, -0.16666666666666666);
+    return fma(x2 * x, q, x);
+}
+static double tire_sin(double z) {
+    if (g_tire_sine && fabs(z) <= 1.5707963267948966) return tire_sin_poly(z);
+    return sin(z);
+}
+double orc_tire_sin(double z) { return tire_sin(z); }
+
 /* mpc_6stati.py:25-53 */
 void orc_tire_forces(const orc_params* p, const double x[6], const double u[2], double out[3]) {
     double vx = x[3], vy = x[4], omega = x[5];
@@ -82,8 +114,8 @@ void orc_tire_forces(const orc_params* p, const double x[6], const double u[2], 
     double alpha_r = atan2(omega * p->lr - vy, vx_eff);
     alpha_f = orc_clamp(alpha_f, -p->maxAlpha, p->maxAlpha);
     alpha_r = orc_clamp(alpha_r, -p->maxAlpha, p->maxAlpha);
-    double Fy_f = p->Df * sin(p->Cf * atan(p->Bf * alpha_f));
-    double Fy_r = p->Dr * sin(p->Cr * atan(p->Br * alpha_r));
+    double Fy_f = p->Df * tire_sin(p->Cf * atan(p->Bf * alpha_f));
+    double Fy_r = p->Dr * tire_sin(p->Cr * atan(p->Br * alpha_r));
     double Frx = (p->Cm1 - p->Cm2 * vx) * d - p->Cr0 - p->Cr2 * (vx * vx);
     out[0] = Fy_f; out[1] = Fy_r; out[2] = Frx;
 }

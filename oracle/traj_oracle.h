@@ -94,6 +94,12 @@ void orc_default_cfg(orc_mpc_cfg* c, int N, double Ts);
 
 double orc_clamp(double x, double lo, double hi);
 void orc_tire_forces(const orc_params* p, const double x[6], const double u[2], double out[3]);
+/* Tire sine evaluation (mpc_6stati.py:46-47): 0 = libm sin (default; the reference fixtures pin it), 1 = the HIP
+ * path's bounded-range polynomial (trajmpc physics.h tire_sin_poly, same coefficients and fma order).  Returns the
+ * previous mode.  Process-global. */
+int orc_set_tire_sine(int mode);
+/* The tire sine in the current mode (for the test that bounds the polynomial against libm). */
+double orc_tire_sin(double z);
 void orc_f_cont(const orc_params* p, const double x[6], const double u[2], double xdot[6]);
 void orc_numerical_jacobian(const orc_params* p, const double x[6], const double u[2],
                             double eps_x, double eps_u, double Jx[36], double Ju[12], double f[6]);

@@ -118,3 +118,26 @@ def test_spawned_worker_failure_stops_the_siblings():
         bench._spawn_workers(2, poll_s=0.05, grace_s=5.0, cmd=[sys.executable, "-c", script])
     assert e.value.code == 3
     assert time.time() - t0 < 20
+
+
+def test_bench_world1_config3_host_io_and_profile_reasons(tmp_path, monkeypatch):
+    """The one-GPU line's extra objects with the CPU stand-in: config3 (configs[2]: N = 40 mixed, the same timed-region
+    contract) with its own roofline, host_io (H2D + run + D2H), the timed-region note, and a profile that does not
+    describe the launch is rejected with the reason recorded instead of a silent null."""
+    import json
+    import bench
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE"):
+        monkeypatch.delenv(k, raising=False)
+    bad = tmp_path / "sq.json"
+    bad.write_text(json.dumps({"batch": 4, "horizon": 20, "f64_flop_issued_per_step": 1.0, "valu_insts_per_step": 1.0}))
+    out = bench.main(["--steps", "3", "--warmup", "1", "--batch", "4", "--dataset-steps", "0", "--no-cpu", "--no-knet",
+                      "--no-config1", "--config3-issue-json", str(bad), "--issue-json", str(bad),
+                      "--traffic-json", str(tmp_path / "none.json")], ops_factory=CpuOps, backend="gloo")
+    assert out["n_gpus"] == 1 and "H2D / D2H excluded" in out["config"]["timed_region"]
+    assert out["roofline"]["issue"] is not None and out["roofline"]["issue"]["source"].endswith("sq.json")
+    assert "not found" in out["roofline"]["traffic_rejected"]
+    c3 = out["config3"]
+    assert c3["config"]["horizon"] == 40 and c3["value"] > 0 and c3["roofline"]["kernel"].startswith("solve_kernel<80")
+    assert c3["roofline"]["issue"] is None and "horizon = 20, this launch has 40" in c3["roofline"]["issue_rejected"]
+    hio = out["host_io"]
+    assert hio["value"] > 0 and hio["steps"] == 4 and hio["d2h_bytes"] == 4 * 5 * 6 * 8 + 4 * 4 * 2 * 8 + 2 * 4 * 4 * 4

@@ -53,6 +53,13 @@ def _same(a, b):
     return torch.equal(a, b)
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _oracle_gpu_tire_sine(oracle_lib):
+    """The oracle gates below run with the HIP path's tire sine (oracle.tire_sine(1); see tests/test_gpu_parity.py)."""
+    with oracle_lib.tire_sine(1):
+        yield
+
+
 def test_configs3_rank_share_through_rccl_gather(gpu, rccl_group, oracle_lib, tmp_path):
     """dataset.generate at configs[3]'s per-rank shape with the RCCL gather:
     * pack -> dist.gather (nccl) -> unpack equals run_closed_loop of the same workload bit for bit;

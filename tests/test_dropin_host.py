@@ -33,3 +33,15 @@ def test_struct_cache_unhashable_builds_fresh():
     s1 = M._cached_struct("cfg", lambda: built.append(1) or TB.config_struct(), object())
     s2 = M._cached_struct("cfg", lambda: built.append(1) or TB.config_struct(), object())
     assert len(built) == 2 and s1 is not s2
+
+
+def test_struct_cache_keys_signed_zeros_and_types_apart():
+    """-0.0 and 0.0 (and 1, 1.0, True) are distinct keys: a cached struct is exactly what config_struct builds for the
+    arguments given (a -0.0 bound is kept as -0.0, which the clamp's sign of zero follows)."""
+    keys = [M._frozen(v) for v in (0.0, -0.0, 1, 1.0, True, np.float32(0.0))]
+    assert len(set(keys)) == 6
+    assert M._frozen(np.float64(-0.0)) == M._frozen(-0.0)   # (a float64 scalar is the same double)
+    a = _cfg(u_bounds=((-1.0, 1.0), (-0.6, 0.0)))
+    b = _cfg(u_bounds=((-1.0, 1.0), (-0.6, -0.0)))
+    assert a is not b
+    assert bytes(b) == bytes(TB.config_struct(N=20, Ts=0.05, u_bounds=((-1.0, 1.0), (-0.6, -0.0))))

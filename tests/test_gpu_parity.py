@@ -33,6 +33,18 @@ TB = pytest.importorskip("trajectory_generation_amd.batch")
 MAX_ITER = 10000   # traj_mpc_config / OSQP max_iter (CVXPY's default)
 
 
+@pytest.fixture(autouse=True, scope="module")
+def _oracle_gpu_tire_sine(oracle_lib):
+    """Every GPU-vs-oracle gate in this module runs the oracle with the HIP path's tire sine (physics.h tire_sin_poly,
+    the same coefficients and fma order: oracle.tire_sine(1)), so the two sides evaluate the same Pacejka physics and
+    an unconverged point (the 10,000-iteration cap) is compared by U like any other.  The polynomial's own distance
+    from libm's sine -- the reference's -- is bounded separately (tests/test_oracle_golden.py
+    test_tire_sine_poly_vs_libm_and_fixtures, <= 2 ulp) and the GPU physics stays gated against the reference
+    fixtures at 1e-12 below."""
+    with oracle_lib.tire_sine(1):
+        yield
+
+
 def rel(a, b):
     return np.max(np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b))))
 
@@ -103,9 +115,9 @@ def _agreement(g, r, both_pol_tol, neither_tol, flag_agree, iters_equal):
     both = pg & pr & ok
     assert du[both].max(initial=0.0) <= both_pol_tol
     # (an instance that ran to the 10,000-iteration cap -- exact mode's continuation round keeps "optimal" there when
-    # the base eps is met -- stopped at no converged point: a 2-ulp change of the tire sine alone moves the oracle's own
-    # cap point by 0.12 at N = 40, so it is compared by status and iteration count only)
-    neither = ~pg & ~pr & (g["status"] == 0) & (g["iters"] < MAX_ITER)
+    # the base eps is met -- is compared by U as well: the oracle evaluates the GPU's tire sine in this module, so a
+    # cap point no longer moves with a 2-ulp change of the sine alone, which shifted one such point by 0.12 at N = 40)
+    neither = ~pg & ~pr & (g["status"] == 0)
     assert du[neither].max(initial=0.0) <= neither_tol
     dobj = np.abs(g["objective"] - r["objective"]) / np.abs(r["objective"])
     assert dobj[both].max(initial=0.0) <= 1e-7
@@ -568,7 +580,7 @@ def test_fused_run_ahead_bit_identical(gpu, levels, grid):
             TB.closed_loop_run(x, u, paths, vr, cfg, None, 0, T0, hx, hu, st[:T0], it[:T0])
             TB.closed_loop_run(x, u, paths, vr, cfg, None, T0, T - T0, hx, hu, st[T0:], it[T0:])
         finally:
-            _lib.lib().traj_debug_run_ahead(4)
+            _lib.lib().traj_debug_run_ahead(0)   # the library default (TGMPC_RUN_AHEAD 0): later tests run the product path
             _lib.lib().traj_debug_fused_grid(0)
         assert _same(hx, per["X"]) and _same(hu, per["U"]), N
         assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"]), N
@@ -662,6 +674,42 @@ def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
     d = M.mpc_step_batch(x0, up, pr_, vr, Ts=Ts, N=N)
     assert np.array_equal(d["status"].cpu().numpy(), g["status"])
     assert np.array_equal(d["u_cmd"].cpu().numpy(), g["u_cmd"])
+
+
+@pytest.mark.parametrize("N,Ts,B", [(48, 0.02, 16), (60, 0.05, 12), (80, 0.02, 6)])
+def test_long_horizon_exact_mode_and_qp_batch_vs_oracle(gpu, oracle_lib, N, Ts, B):
+    """The long-horizon kernel's exact polish (polish_mode 1: the KKT certificate, active-set passes, continuation
+    rounds) against the oracle's, with K^-1 in LDS (N 48, 60) and in the caller's scratch (N 80): statuses identical,
+    the certificate outcome and the iteration counts equal on >= 90 %, U within 1e-6 where both certified and 0.1
+    where neither did (an eps ADMM point, possibly at the iteration cap).  Then the QP entry point
+    (traj_mpc_qp_batch, the caller's A_k, B_k, g_k: here the oracle's own rollout + linearize_discretize,
+    mpc_6stati.py:165-178) at the same horizons in both polish modes against the oracle's step on the same inputs."""
+    g, r = _step_both(oracle_lib, 19, B, N, Ts, 1)
+    assert np.array_equal(g["status"], r["status"])
+    ok = g["status"] <= 1
+    pg, pr = g["polished"] > 0, r["polished"] > 0
+    assert np.mean(pg == pr) >= 0.9 and np.mean(g["iters"] == r["iters"]) >= 0.9
+    du = np.abs(g["U_opt"] - r["U_opt"]).max(axis=(1, 2))
+    assert du[pg & pr & ok].max(initial=0.0) <= 1e-6
+    assert du[~pg & ~pr & ok].max(initial=0.0) <= 1e-1
+    assert (pg & pr & ok).sum() >= 1
+    x0, up, prf, vr = random_instances(19, B, N, Ts)
+    Ad, Bd, gd = np.zeros((B, N, 6, 6)), np.zeros((B, N, 6, 2)), np.zeros((B, N, 6))
+    for b in range(B):
+        xb = oracle_lib.nominal_rollout(x0[b], up[b], N, Ts)
+        for k in range(N):
+            Ad[b, k], Bd[b, k], gd[b, k] = oracle_lib.linearize_discretize(xb[:, k], up[b], Ts)
+    for mode in (0, 1):
+        q = {k: v.cpu().numpy() for k, v in
+             TB.mpc_qp_batch(x0, up, prf, vr, Ad, Bd, gd, TB.config_struct(N=N, Ts=Ts, polish_mode=mode)).items()}
+        ro = oracle_lib.mpc_step_batch(x0, up, prf, vr, oracle_lib.cfg(N=N, Ts=Ts, polish_mode=mode))
+        assert np.array_equal(q["status"], ro["status"]), mode
+        okq = q["status"] <= 1
+        both = okq & (q["polished"] > 0) & (ro["polished"] > 0)
+        assert both.sum() >= 1, mode
+        dq = np.abs(q["U_opt"] - ro["U_opt"]).max(axis=(1, 2))
+        assert dq[both].max(initial=0.0) <= 1e-6, mode
+        assert np.array_equal(q["u_cmd"][okq], q["U_opt"][okq][:, :, 0])
 
 
 @pytest.mark.parametrize("N,Ts", [(8, 0.05), (20, 0.05), (20, 0.02), (30, 0.05), (40, 0.05)])

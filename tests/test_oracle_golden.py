@@ -45,6 +45,32 @@ def test_physics_vs_reference(oracle_lib):
     np.testing.assert_allclose(le, ph["lateral_error"], rtol=1e-14, atol=1e-15)
 
 
+def test_tire_sine_poly_vs_libm_and_fixtures(oracle_lib):
+    """The HIP path's Pacejka sine (physics.h tire_sin_poly, restated in the oracle as tire_sine mode 1) against
+    libm's sine -- the reference's numpy sin: within 2 ulp over the whole range the tire argument C atan(B alpha) can
+    take, libm's own value outside it, and the reference fixtures' tire forces / f to the same 1e-13 / 1e-12 bars as
+    the libm oracle.  This bounds the one physics difference between the GPU and the reference's libm sine; the GPU
+    parity gates run the oracle with the polynomial (tests/test_gpu_parity.py)."""
+    O = oracle_lib
+    z = np.concatenate([np.linspace(-np.pi / 2, np.pi / 2, 200001), np.random.default_rng(0).uniform(-1.6, 1.6, 50000),
+                        [0.0, -0.0, 1e-300, -1e-300, 1e-8, np.pi / 2, -np.pi / 2]])
+    with O.tire_sine(1):
+        sp = O.tire_sin(z)
+        ph = _load("physics")
+        tf = np.array([O.tire_forces(x, u) for x, u in zip(ph["x"], ph["u"])])
+        fc = np.array([O.f_cont(x, u) for x, u in zip(ph["x"], ph["u"])])
+    sl = np.sin(z)
+    ulp = np.spacing(np.abs(sl))
+    inside = np.abs(z) <= np.pi / 2
+    assert (np.abs(sp - sl)[inside] <= 2 * ulp[inside]).all(), (np.abs(sp - sl) / ulp)[inside].max()
+    assert np.array_equal(sp[~inside], sl[~inside])
+    # (z = -0: the polynomial's fma returns +0 where libm returns -0 -- the same zero force; the GPU does the same)
+    assert (sp[z == 0] == 0.0).all()
+    np.testing.assert_allclose(tf, ph["tire_forces"], rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(fc, ph["f_cont"], rtol=1e-12, atol=1e-12)
+    assert O.set_tire_sine(0) == 0   # the context manager restored the default (libm)
+
+
 @pytest.mark.parametrize("N", [20, 40])
 @pytest.mark.parametrize("tag", ["002", "005"])
 def test_nominal_rollout_vs_reference(oracle_lib, N, tag):

@@ -15,13 +15,14 @@
 #   sq          SQ f64 / VALU instruction pass (tools/pmc_f64.py)              -> gpurun_out/$TAG_sq_f64.json
 #   sq40        the same at N = 40                                             -> gpurun_out/$TAG_sq_f64_n40.json
 #   stall       two SQ passes: wave-cycle split, VALU occupancy (tools/pmc_stall.py) -> gpurun_out/$TAG_stall.json
+#   stall40     the same at N = 40 (config 3)                                  -> gpurun_out/$TAG_stall_n40.json
 #   trace       rocprofv3 --kernel-trace --stats of the driver's command + the solve dispatches
 #               (tools/trace_dispatches.py)                                    -> gpurun_out/$TAG_kt/, $TAG_dispatches.json
 #   tiers       horizon tiers: batch (B = 1024) and drop-in per-call times (tools/horizon_tiers.py) -> $TAG_tiers.json
 #   ktraffic    PMC FETCH_SIZE / WRITE_SIZE passes over the FC2 launch alone at B = 1024 in the default mode
 #               (tools/knet_fc2_pmc.py): its HBM bytes (tools/pmc_knet_traffic.py) -> gpurun_out/$TAG_traffic_knet.json
 #   kfc2        PMC passes over FC2 alone in each product mode (tools/pmc_knet_fc2.sh) -> gpurun_out/$TAG_fc2_m*/
-#   ab          A/B of library variants (VARIANTS="v1 v2" under trajectory_generation_amd/_variants/<v>/, built by
+#   ab          A/B of library variants (VARIANTS="v1 v2" under _variants/<v>/, built by
 #               tools/build_variant.sh) against the in-tree build, REPS rounds of CFGS "steps:waves" configurations
 # Environment: TAG (default s5), VARIANTS, REPS, CFGS.  Never kills by pattern; every GPU step has a limit.
 set -o pipefail
@@ -31,7 +32,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-s5}
 O=gpurun_out
 B20="python3 bench.py --steps 20 --warmup 5"
-LEAN="--no-cpu --no-knet --no-config1 --no-cold --dataset-steps 0"
+LEAN="--no-cpu --no-knet --no-config1 --no-cold --dataset-steps 0 --no-config3 --no-host-io"
 N40="--horizon 40 --kind mixed"
 
 pmc_traffic() {   # $1 suffix, $2 extra bench flags, $3 horizon
@@ -42,11 +43,22 @@ pmc_traffic() {   # $1 suffix, $2 extra bench flags, $3 horizon
     python3 tools/pmc_traffic.py --fetch $O/${TAG}_fetch$1 --write $O/${TAG}_write$1 --batch 4096 --horizon $3 \
         --fused-steps 20 --out $O/${TAG}_traffic$1.json > /dev/null
 }
-pmc_sq() {   # $1 suffix, $2 extra bench flags
+pmc_sq() {   # $1 suffix, $2 extra bench flags, $3 horizon
     timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 \
         SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_WAVES -d $O/${TAG}_f64$1 -o run --output-format csv -- \
         $B20 $LEAN $2 > $O/${TAG}_f64$1.log 2>&1 &&
-    python3 tools/pmc_f64.py $O/${TAG}_f64$1 --batch 4096 --steps-per-launch 20 --out $O/${TAG}_sq_f64$1.json > /dev/null
+    python3 tools/pmc_f64.py $O/${TAG}_f64$1 --batch 4096 --steps-per-launch 20 --horizon $3 \
+        --out $O/${TAG}_sq_f64$1.json > /dev/null
+}
+
+pmc_stall() {   # $1 suffix, $2 extra bench flags, $3 horizon: two SQ passes (wave-cycle split, VALU occupancy)
+    timeout -s KILL 150 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS -d $O/${TAG}_stall_a$1 -o run \
+        --output-format csv -- $B20 $LEAN $2 > $O/${TAG}_stall_a$1.log 2>&1 &&
+    timeout -s KILL 150 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_SCA \
+        SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE -d $O/${TAG}_stall_b$1 -o run \
+        --output-format csv -- $B20 $LEAN $2 > $O/${TAG}_stall_b$1.log 2>&1 &&
+    python3 tools/pmc_stall.py $O/${TAG}_stall_a$1 $O/${TAG}_stall_b$1 --horizon $3 --out $O/${TAG}_stall$1.json > /dev/null
 }
 
 for step in "$@"; do
@@ -75,17 +87,10 @@ for step in "$@"; do
         timeout -k 10 150 python3 tools/item_timeline.py 20 5 > $O/${TAG}_timeline20.json 2> $O/${TAG}_timeline.err || exit 1 ;;
     traffic) pmc_traffic "" "" 20 && echo ok || exit 1 ;;
     traffic40) pmc_traffic _n40 "$N40" 40 && echo ok || exit 1 ;;
-    sq) pmc_sq "" "" && echo ok || exit 1 ;;
-    sq40) pmc_sq _n40 "$N40" && echo ok || exit 1 ;;
-    stall)
-        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_LDS -d $O/${TAG}_stall_a -o run \
-            --output-format csv -- $B20 $LEAN > $O/${TAG}_stall_a.log 2>&1 &&
-        timeout -s KILL 120 rocprofv3 --pmc SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_SCA \
-            SQ_INST_CYCLES_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE -d $O/${TAG}_stall_b -o run \
-            --output-format csv -- $B20 $LEAN > $O/${TAG}_stall_b.log 2>&1 &&
-        python3 tools/pmc_stall.py $O/${TAG}_stall_a $O/${TAG}_stall_b --out $O/${TAG}_stall.json > /dev/null \
-            && echo ok || exit 1 ;;
+    sq) pmc_sq "" "" 20 && echo ok || exit 1 ;;
+    sq40) pmc_sq _n40 "$N40" 40 && echo ok || exit 1 ;;
+    stall) pmc_stall "" "" 20 && echo ok || exit 1 ;;
+    stall40) pmc_stall _n40 "$N40" 40 && echo ok || exit 1 ;;
     trace)
         timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/${TAG}_kt -o run --output-format csv -- \
             python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/${TAG}_kt.log 2>&1 &&
@@ -106,7 +111,7 @@ for step in "$@"; do
     ab)
         for rep in $(seq ${REPS:-3}); do
             for v in base $VARIANTS; do
-                if [ "$v" = base ]; then unset TRAJMPC_LIB; else export TRAJMPC_LIB="$PWD/trajectory_generation_amd/_variants/$v/libtrajmpc.so"; fi
+                if [ "$v" = base ]; then unset TRAJMPC_LIB; else export TRAJMPC_LIB="$PWD/_variants/$v/libtrajmpc.so"; fi
                 for c in ${CFGS:-20:0 200:0}; do
                     s=${c%%:*}; w=${c##*:}
                     if [ "$w" = 0 ]; then unset TRAJ_FUSED_WAVES; else export TRAJ_FUSED_WAVES=$w; fi

@@ -1,8 +1,8 @@
 #!/bin/bash
-# KalmanNet bench leg (tools/knet_bench.py) for every library build under trajectory_generation_amd/_variants/*/.
+# KalmanNet bench leg (tools/knet_bench.py) for every library build under _variants/*/.
 cd "$(dirname "$0")/.." || exit 1
 mkdir -p gpurun_out
-for d in trajectory_generation_amd/_variants/*/; do
+for d in _variants/*/; do
   v=$(basename "$d")
   export TRAJMPC_LIB="$PWD/$d/libtrajmpc.so"
   timeout -k 10 200 python tools/knet_bench.py > gpurun_out/kv.json 2>/dev/null || { echo "$v failed"; exit 1; }

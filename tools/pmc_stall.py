@@ -28,12 +28,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--out")
+    ap.add_argument("--horizon", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=4096)
     a = ap.parse_args()
     c = {}
     for d in a.dirs:
         c.update(largest(d))
     w = c.get("SQ_WAVE_CYCLES", 0.0)
-    out = {"counters": dict(c)}
+    out = {"batch": a.batch, "horizon": a.horizon, "counters": dict(c)}
     if w:
         out["share_of_wave_cycles"] = {k: c[k] / w for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
                                                              "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",

@@ -85,13 +85,12 @@
 #define TGMPC_RESMAX2 1        // two-wave residual checks: the maxima by an LDS-transposed reduction (0: block_max)
 #endif
 #ifndef TGMPC_KMC80
-#define TGMPC_KMC80 4          // the same at capacity 80 (one wave per SIMD): 8 measured 0.87 M vs 0.93 M at config 3
-                               // (and with 40-value chunks 0.85 M; round 5, profiles/r05_kmc80_ab_n40.txt)
+#define TGMPC_KMC80 4          // independent FMA chains of the capacity-80 ADMM mat-vec (every capacity-80 instance,
+                               // fused and per-step alike, so they stay bit-identical): 8 measured 0.87 M vs 0.93 M
+                               // at config 3 (and with 40-value chunks 0.85 M; round 5, profiles/r05_kmc80_ab_n40.txt)
 #endif
-#ifndef TGMPC_KMC
-#define TGMPC_KMC 4            // independent FMA chains of the ADMM mat-vec (K^-1 v) at capacity <= 64: 4 or 8 (8 in
-                               // the fused instance measured 9.2-9.5 M vs 13.0-13.5 M steps/s at the driver's command)
-#endif
+// (capacity <= 64 uses 4 chains, fixed: the round-5 build knob for 8 changed only some instances' summation order and
+// so broke the fused / per-step bit-identity; 8 chains had measured 9.2-9.5 M vs 13.0-13.5 M steps/s there anyway)
 #ifndef TGMPC_KCH80
 #define TGMPC_KCH80 40         // capacity 80, one wave per SIMD: broadcast values per chunk of the ADMM mat-vec (round 5,
                                // under the max-ILP scheduler: 40 0.965-0.969 M at config 3, 16 0.952, 80 0.946, 20 0.935,
@@ -1144,11 +1143,11 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
             return own ? ((sa[0] + sa[1]) + (sa[2] + sa[3])) + ((sa[4] + sa[5]) + (sa[6] + sa[7])) : 0.0;
         };
         double Krow[NN];
-        auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, TGMPC_KMC independent FMA chains
-            // (capacity <= 64; 4 at capacity 80.  Round 2 chose 4 -- one wave issues an f64 op about every 8
-            // cycles; 8 chains measured far slower in the fused instance -- TGMPC_KMC)
-            constexpr int KC = NN <= 64 ? TGMPC_KMC : TGMPC_KMC80;
-            static_assert(KC == 4 || KC == 8, "TGMPC_KMC: 4 or 8 chains");
+        auto Kmul = [&](double v, int slot = -1) -> double {  // (K^{-1} v)_t, KC independent FMA chains
+            // (4 at capacity <= 64 -- round 2 chose 4: one wave issues an f64 op about every 8 cycles, 8 chains
+            // measured far slower in the fused instance; TGMPC_KMC80 at capacity 80, default 4)
+            constexpr int KC = NN <= 64 ? 4 : TGMPC_KMC80;
+            static_assert(KC == 4 || KC == 8, "TGMPC_KMC80: 4 or 8 chains");
             double sa[KC];
 #pragma unroll
             for (int i = 0; i < KC; ++i) sa[i] = 0.0;

@@ -245,13 +245,17 @@ static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
     const size_t per = long_ws_doubles(N);
     if (2 * N <= LONG_NKL) {
         const size_t lds = long_lds_bytes(N);
-        static bool attr = false;   // (per process: the attribute is a property of the function)
-        if (!attr) {
+        // the dynamic-LDS attribute is set once per device (it belongs to the function's per-device code object); the
+        // flags are atomics, so concurrent callers on several host threads at worst set it twice
+        static std::atomic<bool> attr[64];
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return TRAJ_E_LAUNCH;
+        if (dev < 0 || dev >= 64 || !attr[dev].load(std::memory_order_acquire)) {
             if (hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_long_kernel<true>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(LONG_NKL * LONG_NKL * sizeof(double))) != hipSuccess)
                 return TRAJ_E_LAUNCH;
-            attr = true;
+            if (dev >= 0 && dev < 64) attr[dev].store(true, std::memory_order_release);
         }
         hipLaunchKernelGGL(solve_long_kernel<true>, dim3(a.B), dim3(LONG_NT), lds, st, a, lws, per);
     } else {

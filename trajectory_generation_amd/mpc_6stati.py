@@ -30,6 +30,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import struct
+
 import numpy as np
 import torch
 
@@ -104,15 +106,17 @@ _STRUCT_CACHE: dict = {}
 
 def _frozen(v):
     """A hashable, exact key for an mpc_step argument (arrays by shape and bytes), or None when there is none."""
-    if v is None or isinstance(v, (bool, int, float, str)):
-        return ("s", v)
+    if v is None or isinstance(v, (bool, int, str)):
+        return ("s", type(v).__name__, v)   # (by type: 1, 1.0 and True hash alike but are different arguments)
+    if isinstance(v, float):
+        return ("f", struct.pack("<d", v))  # by bits: -0.0 and 0.0 (and NaN payloads) are distinct keys
     if isinstance(v, np.ndarray):
         return ("a", v.shape, v.dtype.str, v.tobytes())
     if isinstance(v, (tuple, list)):
         parts = tuple(_frozen(e) for e in v)
         return None if any(e is None for e in parts) else ("t", parts)
     if isinstance(v, np.generic):
-        return ("s", v.item())
+        return ("g", v.dtype.str, v.tobytes())
     return None
 
 
