@@ -96,15 +96,21 @@ typedef struct {
 
 /* Horizon tiers (mpc_step takes any N, mpc_6stati.py:125):
  *   N <= TRAJ_MAX_N (40)                 the register-resident hot kernels (mpc_solve.h): every entry point;
- *   TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG    without state bounds: the long-horizon kernel (mpc_long.h: the hot kernels'
+ *   TRAJ_MAX_N < N <= TRAJ_MAX_N_SPLIT   without state bounds: the row-split kernel (mpc_split.h: K^-1 in registers, each
+ *                                        row split across a lane pair joined by v_permlane32_swap, 2 waves per SIMD);
+ *   TRAJ_MAX_N_SPLIT < N <= TRAJ_MAX_N_LONG  without state bounds: the long-horizon kernel (mpc_long.h: the hot kernels'
  *                                        algorithm with one thread per QP variable, K^-1 in LDS up to N = 64 and in
  *                                        the caller's scratch beyond);
  *   otherwise (state bounds, or N > TRAJ_MAX_N_LONG up to TRAJ_MAX_N_GENERAL) the general condensed-QP solver
  *                                        (mpc_general.h, one 256-thread workgroup per instance, its Cholesky factor
  *                                        in the caller's scratch).
- * Past TRAJ_MAX_N only the step and QP entry points run (traj_mpc_step_batch / traj_mpc_qp_batch, the scratch of
- * traj_mpc_sb_workspace_bytes); the closed-loop entry points return TRAJ_E_UNSUPPORTED. */
+ * Past TRAJ_MAX_N the step and QP entry points take the scratch of traj_mpc_sb_workspace_bytes; the closed-loop entry
+ * points (traj_closed_loop_step / _run) run TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG on the long-horizon kernel, one step per
+ * launch sequence (rollout, Jacobians, the closed-loop long-horizon solve with the window, warm rho and plant update),
+ * with the same extra scratch after the workspace; past TRAJ_MAX_N_LONG, or with state bounds, they return
+ * TRAJ_E_UNSUPPORTED (main.py passes no state bounds). */
 #define TRAJ_MAX_N 40
+#define TRAJ_MAX_N_SPLIT 64      /* TRAJ_MAX_N < N <= this: the row-split kernel (mpc_split.h), K^-1 in registers */
 #define TRAJ_MAX_N_LONG 128
 #define TRAJ_MAX_N_GENERAL 256
 
@@ -135,7 +141,8 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
  * (x_k, f_k) per stage (B * N * 12 doubles), then the closed-loop record of the previous step
  * (B * 4 doubles: rho, valid flag, ADMM iterations, mean iterations of the last fused run), the
  * closed-loop solve order (B ints, longest first) and the fused run's step queue (B + 2 ints).  Pass the same buffer to every traj_closed_loop_step of one run;
- * step t = 0 starts cold. */
+ * step t = 0 starts cold.  The closed loop at TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG needs traj_mpc_workspace_bytes(B, N) +
+ * traj_mpc_sb_workspace_bytes(B, N) bytes (the long-horizon kernel's scratch after the workspace). */
 size_t traj_mpc_workspace_bytes(int B, int N);
 /* Scratch of the general solver, which runs with state bounds (x_lo / x_hi given with a finite side,
  * mpc_6stati.py:208-213), and of the long-horizon kernel (every horizon N > TRAJ_MAX_N): B * ~20.5k doubles at
@@ -181,7 +188,7 @@ typedef struct {
 int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, const double* x_start,
                           const double* vref, double* path_ref, void* stream);
 
-/* One closed-loop step of main.py:85-101 for B trajectories, in place:
+/* One closed-loop step of main.py:85-101 for B trajectories, in place (1 <= N <= TRAJ_MAX_N_LONG, no state bounds):
  *   path_ref = window(x[:,0]); u_cmd = mpc_step(x, u_prev, path_ref, vref); x += Ts f_cont(x, u_cmd);
  *   u_prev = u_cmd.   x [B,6], u_prev [B,2] are updated; vref [B,N+1].
  * If hist_x / hist_u are non-NULL the new state / command are also written to
@@ -269,6 +276,10 @@ int traj_debug_kernel_times(double* ms, int* n_steps);
 /* traj_mpc_step_batch's linearization: 1 (default) inside the solve launch (one launch per call), 0 = the
  * rollout and Jacobian kernels before it.  Results do not depend on it (bit-identical).  For tests. */
 int traj_debug_step_linearize(int in_kernel);
+/* Horizons TRAJ_MAX_N < N <= n_max run the row-split kernel (default TRAJ_MAX_N_SPLIT), the rest of the long tier the
+ * long-horizon kernel (0: every N > TRAJ_MAX_N on the long-horizon kernel).  Both restate the same solver; for the
+ * tests that compare them.  Diagnostics only. */
+int traj_debug_split_max_n(int n_max);
 
 #ifdef __cplusplus
 }

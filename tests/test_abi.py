@@ -192,12 +192,23 @@ def test_argument_errors_are_reported_before_any_launch(L):
     ps.kmax, ps.kind, ps.pc = 0, 16, 16                      # never dereferenced at B = 0
     assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 0, nul, nul, nul, 0, 0, nul, nul, nul,
                                    nul, nul, 0, nul) == _lib.TRAJ_E_UNSUPPORTED
-    # a horizon past the hot kernels' capacity: the closed loop reports it as unsupported, not as an argument error
+    # horizons past the hot kernels' capacity: the closed loop takes them up to TRAJ_MAX_N_LONG (the long-horizon
+    # kernel, whose scratch follows the workspace -- a workspace without it is an argument error before any launch);
+    # past that, or with state bounds, it reports them as unsupported, not as an argument error
     cL = _lib.default_config(60, 0.05)
+    cG = _lib.default_config(_lib.MAX_N_LONG + 1, 0.05)
+    cLx = _lib.default_config(60, 0.05)
+    cLx.has_x_lo, cLx.x_lo[3] = 1, -1.0
+    wsL = L.traj_mpc_workspace_bytes(4, 60)
     for fn in (L.traj_closed_loop_step, L.traj_closed_loop_run):
         extra = (0, 1) if fn is L.traj_closed_loop_run else (0,)
         assert fn(C.byref(p), C.byref(cL), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
-                  nul) == _lib.TRAJ_E_UNSUPPORTED
+                  nul) == _lib.TRAJ_OK
+        assert fn(C.byref(p), C.byref(cL), C.byref(ps), 4, fake, fake, fake, *extra, 0, nul, nul, nul, nul, fake, wsL,
+                  nul) == _lib.TRAJ_E_ARG
+        for cu in (cG, cLx):
+            assert fn(C.byref(p), C.byref(cu), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
+                      nul) == _lib.TRAJ_E_UNSUPPORTED
 
 
 def test_check_raises():

@@ -344,7 +344,7 @@ def test_closed_loop_per_step_parity_ts005(gpu, oracle_lib, kind, N, T, B, warm)
         assert n_it / n >= 0.95
 
 
-@pytest.mark.parametrize("kind,N,T,B", [("spline", 20, 20, 48), ("mixed", 40, 20, 32)])
+@pytest.mark.parametrize("kind,N,T,B", [("spline", 20, 20, 48), ("mixed", 40, 20, 32), ("mixed", 48, 12, 16)])
 def test_closed_loop_warm_rho_per_step_vs_warm_oracle(gpu, oracle_lib, kind, N, T, B):
     """The warm-started closed loop (the bench line's semantics: each instance starts its ADMM from the rho its
     previous step adapted to, x = z = y = 0 as cold) gated step by step against the oracle run with the SAME warm
@@ -370,7 +370,7 @@ def test_closed_loop_warm_rho_per_step_vs_warm_oracle(gpu, oracle_lib, kind, N, 
     hx[:, 0] = x
     st = torch.empty((T, B), dtype=torch.int32, device=dev)
     it = torch.empty((T, B), dtype=torch.int32, device=dev)
-    ws = TB.workspace(B, N, dev)
+    ws = TB.workspace(B, N, dev, TB._closed_extra(B, N))   # (the closed loop's own buffer: past N = 40 with its scratch)
     off = 66 * B * N   # the warm records: 4 doubles per instance after A, B, g and the stage records (trajmpc.hip)
     ocfg = oracle_lib.cfg(N=N, Ts=Ts)
     vr = np.tile(w["vref"], (B, 1))
@@ -994,3 +994,64 @@ def test_divergent_dataset_trajectory_step_gate(gpu, oracle_lib):
         assert du[eq].max(initial=0.0) <= 1e-3, (t, du)
         n_cmp += int(both.sum() + eq.sum())
     assert n_cmp >= 200
+
+
+# ------------------------------------------------------------------ the closed loop past N = 40 (long-horizon kernel)
+
+@pytest.mark.parametrize("kind,N,Ts,T,B,warm", [("spline", 60, 0.05, 10, 16, 0), ("mixed", 48, 0.05, 10, 16, 0),
+                                                ("spline", 60, 0.02, 12, 16, 0), ("spline", 100, 0.05, 4, 6, 0)])
+def test_closed_loop_long_horizon_per_step(gpu, oracle_lib, kind, N, Ts, T, B, warm):
+    """MPC/main.py's loop at horizons past the register-resident capacity (mpc_step takes any N, mpc_6stati.py:125;
+    the closed loop runs the long-horizon kernel one step per launch sequence, include/trajmpc.h tiers).  SURVEY.md
+    8(d) gate (1), at Ts = 0.05 and at main.py's Ts = 0.02 too: at N = 60 whole trajectories are no gate even at
+    Ts = 0.02 -- the oracle's own closed loop with libm's and with the polynomial tire sine separates by 0.32 over 40
+    steps there (eps = 1e-5 ADMM points amplified over the 60-stage preview) -- so every step of the GPU closed loop is re-solved from the GPU's own state by the step
+    entry point (bit-identical to what the loop applied when warm start is off) and by the oracle (with the same
+    carried rho when it is on): statuses identical, u to 1e-6 where both polished, to 1e-3 where both stopped
+    unpolished at the same iteration, iteration counts equal on >= 95 %.  The fused entry point (traj_closed_loop_run)
+    equals the per-step launches bit for bit.  N 48 / 60 run the row-split kernel (mpc_split.h), N = 100 the long-horizon
+    one; the warm-started loop past N = 40 is gated in test_closed_loop_warm_rho_per_step_vs_warm_oracle."""
+    from trajectory_generation_amd.workload import make_workload
+    w = make_workload(B, N, Ts, kind=kind, seed=21)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=warm)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    fus = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=True)
+    for k in ("X", "U", "status", "iters"):
+        assert _same(per[k], fus[k]), k
+    res = {k: v.cpu().numpy() for k, v in per.items()}
+    vr = np.tile(w["vref"], (B, 1))
+    rho, valid = np.full(B, 0.1), np.zeros(B, np.int32)
+    n = n_it = n_pol = n_close = 0
+    for t in range(T):
+        xt = res["X"][:, t]
+        ut = res["U"][:, t - 1] if t > 0 else np.asarray(w["u0"])
+        prt = TB.ref_window_batch(paths, xt[:, 0], vr, N, Ts).cpu().numpy()
+        if not warm:
+            g = {k: v.cpu().numpy() for k, v in TB.mpc_step_batch(xt, ut, prt, vr, cfg).items()}
+            assert np.array_equal(g["u_cmd"], res["U"][:, t]) and np.array_equal(g["status"], res["status"][t])
+            assert np.array_equal(g["iters"], res["iters"][t])
+            ro = oracle_lib.mpc_step_batch(xt, ut, prt, vr, oracle_lib.cfg(N=N, Ts=Ts))
+        else:
+            ro = oracle_lib.mpc_step_batch_warm(xt, ut, prt, vr, rho, valid, oracle_lib.cfg(N=N, Ts=Ts, warm_start=1))
+            rho, valid = ro["rho"], ro["valid"]
+        assert np.array_equal(res["status"][t], ro["status"]), (t, res["status"][t], ro["status"])
+        ok = res["status"][t] <= 1
+        du = np.abs(res["U"][:, t] - ro["u_cmd"]).max(axis=1)
+        it_eq = res["iters"][t] == ro["iters"]
+        pr_ = ro["polished"] > 0
+        if not warm:
+            # the step entry point's polish flag: where both polished the optimum agrees, where neither did the eps
+            # ADMM points agree at the same stopping iteration, and the polish outcome agrees but for borderline flips
+            pg = g["polished"] > 0
+            assert du[pg & pr_ & ok].max(initial=0.0) <= 1e-6, (t, du)
+            assert du[~pg & ~pr_ & it_eq & ok].max(initial=0.0) <= 1e-3, (t, du)
+            n_pol += int((pg == pr_).sum())
+        else:
+            # (no polish flag from the closed loop: u within 1e-6 where the oracle polished on >= 95 %, all within 1e-2)
+            n_pol += int(((du <= 1e-6) | ~pr_ | ~ok).sum())
+            assert du[ok].max(initial=0.0) <= 1e-2, (t, du)
+        n_close += int((du[ok] <= 1e-3).sum() + (~ok).sum())
+        n_it += int(it_eq.sum())
+        n += B
+    assert n_it / n >= 0.95 and n_pol / n >= 0.95 and n_close / n >= 0.98, (n_it / n, n_pol / n, n_close / n)

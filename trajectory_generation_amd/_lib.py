@@ -18,6 +18,7 @@ HEADERS = [HEADER, os.path.join(os.path.dirname(_HERE), "include", "trajknet.h")
 
 TRAJ_OK, TRAJ_E_ARG, TRAJ_E_UNSUPPORTED, TRAJ_E_LAUNCH, TRAJ_E_HANDOFF = 0, -1, -2, -3, -4
 MAX_N = 40            # hot kernels, every entry point (include/trajmpc.h TRAJ_MAX_N)
+MAX_N_SPLIT = 64      # the row-split kernel for MAX_N < N <= MAX_N_SPLIT (TRAJ_MAX_N_SPLIT)
 MAX_N_LONG = 128      # step / QP entry points on the long-horizon kernel without state bounds (TRAJ_MAX_N_LONG)
 MAX_N_GENERAL = 256   # step / QP entry points on the general solver (TRAJ_MAX_N_GENERAL)
 
@@ -114,6 +115,7 @@ _SIGS = {
     "traj_debug_run_ahead": (C.c_int, [C.c_int]),
     "traj_debug_fused_waves": (C.c_int, [C.c_int]),
     "traj_debug_step_linearize": (C.c_int, [C.c_int]),
+    "traj_debug_split_max_n": (C.c_int, [C.c_int]),
     "traj_debug_set_item_stamps": (C.c_int, [_V]),
     "traj_closed_loop_check": (C.c_int, [_V, C.c_size_t, C.c_int, C.c_int, _V]),
     "traj_dataset_write_csv": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_double, _V, _V, _V, _V,

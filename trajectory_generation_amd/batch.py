@@ -322,13 +322,19 @@ def ref_window_batch(paths: PathSet, x_start, vref, N, Ts) -> torch.Tensor:
     return out
 
 
+def _closed_extra(B: int, N: int) -> int:
+    """The closed loop past the register-resident capacity (MAX_N < N <= MAX_N_LONG) runs the long-horizon kernel one
+    step per launch sequence; its scratch follows the workspace (traj_mpc_sb_workspace_bytes), as for the step."""
+    return int(_lib.lib().traj_mpc_sb_workspace_bytes(int(B), int(N))) if N > _lib.MAX_N else 0
+
+
 def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None, t=0, hist_x=None, hist_u=None,
                      status=None, iters=None):
     """One step of MPC/main.py:85-101 for all B trajectories; x [B,6], u_prev [B,2] updated in place."""
     B = x.shape[0]
     ps = paths.struct()
     T = hist_u.shape[1] if hist_u is not None else 0
-    ws = workspace(B, cfg.N, x.device)
+    ws = workspace(B, cfg.N, x.device, _closed_extra(B, cfg.N))
     _lib.check(_lib.lib().traj_closed_loop_step(
         C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t), int(T),
         _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()), "traj_closed_loop_step")
@@ -342,7 +348,7 @@ def closed_loop_run(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None
     B = x.shape[0]
     ps = paths.struct()
     T = hist_u.shape[1] if hist_u is not None else 0
-    ws = workspace(B, cfg.N, x.device)
+    ws = workspace(B, cfg.N, x.device, _closed_extra(B, cfg.N))
     _lib.check(_lib.lib().traj_closed_loop_run(
         C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t0),
         int(steps), int(T), _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()),

@@ -10,6 +10,10 @@
 //     polish with its KKT certificate), as the CPU oracle under oracle/ restates them;
 //   * K = P + sigma I + A' diag(rho) A is inverted explicitly by the symmetric sweep operator (n pivots), so every
 //     ADMM iteration is one dense mat-vec -- as in the hot kernel.
+// CLOSED: one closed-loop step of MPC/main.py:85-101 (traj_closed_loop_step / _run past TRAJ_MAX_N): the state and
+// u_prev from the closed-loop buffers, the reference window from the state (main.py:51-68, as mpc_solve.h does), the
+// warm-start rho carried in the workspace's warm record, and the plant update x <- x + Ts f(x, u_cmd) (:97), u_prev
+// <- u_cmd (:101) with the history, instead of X_opt / U_opt / the objective.
 // Layout: one 256-thread workgroup per instance, thread t owns variable t (n <= 256).  The scaled P lives in the
 // caller's scratch, COLUMN-major (entry (r, j) at j ld + r: for fixed j the threads read consecutive doubles), ld x ld
 // with ld = n rounded up to 8 and zero padding; K^-1 the same way, in LDS (dynamic shared memory, n <= LONG_NKL:
@@ -37,7 +41,7 @@ __host__ inline size_t long_lds_bytes(int N) {
     return n <= LONG_NKL ? (size_t)long_ld(n) * long_ld(n) * sizeof(double) : 0;
 }
 
-template <bool KL>
+template <bool KL, bool CLOSED = false>
 __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, double* lws, size_t lstride) {
     extern __shared__ __attribute__((aligned(16))) double s_kl[];   // K^-1 (KL)
     __shared__ double s_bc[2][LONG_NT];       // broadcast vectors (rotating)
@@ -47,6 +51,9 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
     __shared__ double s_F[3][LONG_NT];        // condensing: F_k rows
     __shared__ double s_red[4 * 8];
     __shared__ int s_flag[4];
+    // CLOSED: the step's state, u_prev and reference window (main.py:51-68) -- x_state / u_state are overwritten by the
+    // plant update at the end, so every read goes through these copies
+    __shared__ double s_xc[CLOSED ? 6 : 1], s_uc[CLOSED ? 2 : 1], s_prc[CLOSED ? 3 * (LONG_NT / 2 + 1) : 1];
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
@@ -100,10 +107,33 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         }
         return m;
     };
-    const double* x0 = a.x0 + 6 * (size_t)b;
-    const double* up = a.u_prev + 2 * (size_t)b;
-    const double* pref = a.path_ref + (size_t)3 * (N + 1) * b;
     const double* vr = a.vref + (size_t)(N + 1) * b;
+    if constexpr (CLOSED) {
+        if (t < 6) s_xc[t] = a.x_state[6 * (size_t)b + t];
+        if (t < 2) s_uc[t] = a.u_state[2 * (size_t)b + t];
+        __syncthreads();
+        // main.py:51-68: xs_0 = X, xs_{k+1} = xs_k + vref_k Ts (serial, as ref_window_kernel / mpc_solve.h); ys = path(xs),
+        // phi* = atan(path'(xs))
+        if (t == 0) {
+            double xs = s_xc[0];
+            s_prc[0] = xs;
+            for (int k = 0; k < N; ++k) {
+                xs = xs + vr[k] * c.Ts;
+                s_prc[3 * (k + 1)] = xs;
+            }
+        }
+        __syncthreads();
+        for (int k = t; k <= N; k += LONG_NT) {
+            double y, dy;
+            path_eval(a.path, b, s_prc[3 * k], y, dy);
+            s_prc[3 * k + 1] = y;
+            s_prc[3 * k + 2] = pm_atan(dy);
+        }
+        __syncthreads();
+    }
+    const double* x0 = CLOSED ? s_xc : a.x0 + 6 * (size_t)b;
+    const double* up = CLOSED ? s_uc : a.u_prev + 2 * (size_t)b;
+    const double* pref = CLOSED ? s_prc : a.path_ref + (size_t)3 * (N + 1) * b;
     const double* gA = a.Ad + (size_t)36 * N * b;
     const double* gB = a.Bd + (size_t)12 * N * b;
     const double* gg = a.gd + (size_t)6 * N * b;
@@ -356,6 +386,12 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         constexpr int PH_ADMM = 0, PH_POLISH = 1, PH_DONE = 2;
         int phase = PH_ADMM;
         double rho = c.rho;
+        // closed-loop warm start (t > 0): the rho the instance's previous step adapted to (mpc_solve.h, the oracle's
+        // orc_warm); iterates start at zero as cold
+        if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {
+            const double* wv = a.wsWarm + 4 * (size_t)b;
+            if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
+        }
         double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
         Res r = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -575,9 +611,19 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         }
         if (iter > c.max_iter) iter = c.max_iter;
         xsol = D * x;
+        if (CLOSED && a.wsWarm && t == 0) {
+            double* wv = a.wsWarm + 4 * (size_t)b;
+            wv[0] = rho;
+            wv[1] = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE) ? 1.0 : 0.0;
+            wv[2] = (double)iter;
+        }
     } else {
         status = early;
         iter = 0;
+        if (CLOSED && a.wsWarm && t == 0) {
+            a.wsWarm[4 * (size_t)b + 1] = 0.0;
+            a.wsWarm[4 * (size_t)b + 2] = 0.0;
+        }
     }
 
     // ---- outputs (:257-275): U, X_opt by the linear model, the objective, u_cmd ----
@@ -588,6 +634,30 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
     Ub[t] = own ? xsol : 0.0;
     if (t < 6) s_xh[t] = x0[t];
     __syncthreads();
+    if constexpr (CLOSED) {
+        // plant x <- x + Ts f(x, u_cmd) (main.py:97), u_prev <- u_cmd (:101); the history and this step's outcome
+        // (main.py:94 keeps only u_cmd: no X_opt, no objective)
+        if (t == 0) {
+            const double uc0 = good ? Ub[0] : up[0], uc1 = good ? Ub[1] : up[1];
+            double xs[6], f[6], u[2] = {uc0, uc1};
+            for (int i = 0; i < 6; ++i) xs[i] = x0[i];
+            f_cont(p, xs, u, f);
+            for (int i = 0; i < 6; ++i) {
+                const double xn = xs[i] + c.Ts * f[i];
+                a.x_state[6 * (size_t)b + i] = xn;
+                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + a.t + 1) * 6 + i] = xn;
+            }
+            a.u_state[2 * (size_t)b] = uc0;
+            a.u_state[2 * (size_t)b + 1] = uc1;
+            if (a.hist_u) {
+                a.hist_u[((size_t)b * a.hist_T + a.t) * 2] = uc0;
+                a.hist_u[((size_t)b * a.hist_T + a.t) * 2 + 1] = uc1;
+            }
+            if (a.status) a.status[b] = status;
+            if (a.iters) a.iters[b] = iter;
+        }
+        return;
+    }
     // X_{k+1} = A_k X_k + B_k U_k + g_k, stage by stage (thread r < 6: state r); X in s_ex (6 (N+1) <= 4 * 256)
     double* const Xs = &s_ex[0][0];
     if (t < 6) Xs[t] = x0[t];

@@ -1,0 +1,816 @@
+// mpc_split.h -- the MPC step with the KKT inverse ROW-SPLIT across lane pairs, register resident: TRAJ_MAX_N < N <=
+// TRAJ_MAX_N_SPLIT (n = 2N <= 128 QP variables), no state bounds.
+//
+// Reference: MPC/mpc_6stati.py:120-275 (mpc_step takes any N, :125) and, CLOSED, one step of MPC/main.py:85-101.  The
+// algorithm is the hot kernels' and the long-horizon kernel's (mpc_solve.h, mpc_long.h): the condensed QP over U, box +
+// rate rows owned by the variables (A bidiagonal, every product with A or A' a +-2 neighbour exchange), OSQP 0.6's ADMM
+// (Ruiz + cost scaling, sigma / alpha, adaptive rho, OSQP termination) and polish (mode 0: OSQP's reduced KKT and
+// acceptance rule; mode 1: the exact active-set polish with its KKT certificate), as oracle/ restates them; the KKT
+// matrix inverted explicitly by the symmetric sweep operator so that each ADMM iteration is one dense mat-vec.
+//
+// What changes is where K^-1 lives.  The long-horizon kernel keeps it in LDS (one thread per row, every pivot and every
+// mat-vec a read-modify-write of the whole matrix through the LDS pipe, one instance per CU at n > 64).  Here row r of
+// K^-1 is held in REGISTERS by two lanes of one wave, lane l and l + 32 (l = r mod 32, wave r / 32): lane half h holds
+// columns [h H, h H + H), H = capacity / 2 -- 64 doubles (128 VGPRs) at n = 128, so a row fits beside the solver's state
+// in the 256 registers of two waves per SIMD.  The halves are joined by v_permlane32_swap (both lanes then hold the
+// same bits: a sum of two partials is commutative), never through LDS:
+//   * K^-1 v: each lane forms its half's partial sum (4 FMA chains), one swap, one add;
+//   * the sweep's pivot column entry K_rp: the lane half holding column p has it in register 0 (the rows are ROTATED
+//     one register per pivot, so the pivot column is always register 0 of its half; after all 2H pivots -- the padding
+//     ones are a plain rotation -- the order is the identity again), the other half takes it across the swap;
+//   * row maxima (Ruiz norms) and the final sums the same way.
+// Per-row scalar state (the ADMM iterate, the scaling, the bounds) is held by both lanes of a row, computed identically.
+// The scaled P lives in the caller's scratch (row-major, row r's halves contiguous) and is read for residual checks and
+// polish only.  CLOSED: as mpc_long.h (window from the state, warm rho, plant update, history).
+#pragma once
+#include "mpc_common.h"
+
+namespace tgmpc {
+
+// capacities built: H = 48 (n <= 96, 3 waves) and H = 64 (n <= 128, 4 waves)
+template <int H> struct SplitCfg {
+    static constexpr int NR = 2 * H;                 // rows = columns capacity
+    static constexpr int WAVES = (NR + 31) / 32;     // 32 rows per wave
+    static constexpr int NT = 64 * WAVES;
+    static constexpr int NRW = 32 * WAVES;           // row slots (>= NR)
+};
+__host__ __device__ inline int split_h(int n) { return n <= 96 ? 48 : 64; }
+// per-instance scratch (doubles): the scaled P, NRW rows x 2H
+__host__ __device__ inline size_t split_ws_doubles(int N) {
+    const int H = split_h(2 * N);
+    return (size_t)(32 * ((2 * H + 31) / 32)) * (2 * H);
+}
+
+// partner lane's value (lane ^ 32) and the pair sum (the same bits on both lanes)
+__device__ __forceinline__ void swap32(double v, double& mine_lo_half, double& mine_hi_half) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const auto rl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    // after the swap: element 0 holds lanes 0-31 = v[0..31] and lanes 32-63 = v[0..31]; element 1 holds lanes 0-31 =
+    // v[32..63] and lanes 32-63 = v[32..63].  So [0] is the half-0 value and [1] the half-1 value of the row, on both.
+    mine_lo_half = __hiloint2double(rh[0], rl[0]);
+    mine_hi_half = __hiloint2double(rh[1], rl[1]);
+}
+__device__ __forceinline__ double pair_sum(double v) {
+    double a, b;
+    swap32(v, a, b);
+    return a + b;   // (half 0's partial + half 1's partial, the same operands in the same order on both lanes)
+}
+__device__ __forceinline__ double pair_max(double v) {   // NaN-propagating
+    double a, b;
+    swap32(v, a, b);
+    return (a > b || a != a) ? a : b;
+}
+
+template <int H, bool CLOSED = false>
+__global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void solve_split_kernel(const KArgs a, double* sws, size_t sstride) {
+    using SC = SplitCfg<H>;
+    constexpr int NR = SC::NR, NT = SC::NT, NRW = SC::NRW, WAVES = SC::WAVES;
+    constexpr int PL = 2 * H;                 // P row stride (doubles)
+    constexpr int SPV = 2 * H + 2;            // one pivot-row slice buffer: [off + m], m < 2H, off in {0, 1}
+    __shared__ __attribute__((aligned(16))) double s_bc[2][NRW];       // broadcast vectors (rotating)
+    __shared__ double s_ex[4][NRW];                                    // +-2 exchanges (rotating)
+    __shared__ __attribute__((aligned(16))) double s_pv[2][2][SPV];    // sweep: [pivot parity][half][slice]
+    __shared__ __attribute__((aligned(16))) double s_F[3][NRW];        // condensing: F_k rows
+    __shared__ double s_red[WAVES * 8];
+    __shared__ int s_flag[4];
+    __shared__ double s_xc[CLOSED ? 6 : 1], s_uc[CLOSED ? 2 : 1], s_prc[CLOSED ? 3 * (NR / 2 + 1) : 1];
+    __shared__ double s_xs[6 * (NR / 2 + 1)];                          // outputs: X by the linear model
+    __shared__ double s_lin[54 * (NR / 2)];                            // A_k | B_k | g_k of every stage (condensing)
+    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    const int r = 32 * wid + (lane & 31), h = lane >> 5;    // row, half
+    const traj_vehicle_params& p = a.p;
+    const traj_mpc_config& c = a.c;
+    const int N = c.N, n = 2 * N;
+    const bool own = r < n;
+    const int kk = r >> 1, ch = r & 1;
+    double* const Pg = sws + (size_t)b * sstride;            // scaled P, row r at Pg + r PL
+    const double* vr = a.vref + (size_t)(N + 1) * b;
+
+    // ---- block helpers ----
+    int xb = 0, bb = 0;
+    auto exch = [&](double v, int delta) -> double {   // value of row r + delta (0 outside 0..n-1)
+        double* buf = s_ex[xb & 3];
+        xb++;
+        if (h == 0) buf[r] = v;
+        __syncthreads();
+        const int s = r + delta;
+        return (own && s >= 0 && s < n) ? buf[s] : 0.0;
+    };
+    auto bcast = [&](double v) -> const double* {
+        double* buf = s_bc[bb & 1];
+        bb++;
+        if (h == 0) buf[r] = own ? v : 0.0;
+        __syncthreads();
+        return buf;
+    };
+    // Block reductions over DPP (wave_max_dpp / wave_sum_dpp: no per-lane shuffle addresses, which the compiler would
+    // hoist out of the solver's loops and keep live -- spilled -- across the whole solve), then the waves in order.
+    // block max of V values >= 0, NaN propagating (uniform; both halves hold the same per-row values, duplicates are
+    // harmless in a max)
+    auto nmax = [](double x_, double y_) { return (x_ > y_ || x_ != x_) ? x_ : y_; };
+    auto block_max = [&](auto& v) {
+        constexpr int V = sizeof(v) / sizeof(double);
+        static_assert(V <= 8, "s_red");
+        wave_max_dpp<V>(v);
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < V; ++i) s_red[wid * 8 + i] = v[i];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            double m = s_red[i];
+            for (int w = 1; w < WAVES; ++w) m = nmax(m, s_red[w * 8 + i]);
+            v[i] = m;
+        }
+        __syncthreads();
+    };
+    // block sum of the rows' values (half-0 lanes) in a fixed order: the DPP pattern per wave, then the waves in order
+    auto block_sum = [&](double v) -> double {
+        v = wave_sum_dpp((h == 0) ? v : 0.0);
+        if (lane == 0) s_red[wid * 8] = v;
+        __syncthreads();
+        double s = 0.0;
+        for (int w = 0; w < WAVES; ++w) s += s_red[w * 8];
+        __syncthreads();
+        return s;
+    };
+
+    // ---- inputs (:144-163 normalisation by the caller; CLOSED: state, u_prev and the window) ----
+    if constexpr (CLOSED) {
+        if (t < 6) s_xc[t] = a.x_state[6 * (size_t)b + t];
+        if (t < 2) s_uc[t] = a.u_state[2 * (size_t)b + t];
+        __syncthreads();
+        if (t == 0) {   // main.py:51-68: xs_{k+1} = xs_k + vref_k Ts (serial, as ref_window_kernel)
+            double xs = s_xc[0];
+            s_prc[0] = xs;
+            for (int k = 0; k < N; ++k) {
+                xs = xs + vr[k] * c.Ts;
+                s_prc[3 * (k + 1)] = xs;
+            }
+        }
+        __syncthreads();
+        for (int k = t; k <= N; k += NT) {
+            double y, dy;
+            path_eval(a.path, b, s_prc[3 * k], y, dy);
+            s_prc[3 * k + 1] = y;
+            s_prc[3 * k + 2] = pm_atan(dy);
+        }
+    }
+    const double* x0 = CLOSED ? s_xc : a.x0 + 6 * (size_t)b;
+    const double* up = CLOSED ? s_uc : a.u_prev + 2 * (size_t)b;
+    const double* pref = CLOSED ? s_prc : a.path_ref + (size_t)3 * (N + 1) * b;
+    const double* gA = a.Ad + (size_t)36 * N * b;
+    const double* gB = a.Bd + (size_t)12 * N * b;
+    const double* gg = a.gd + (size_t)6 * N * b;
+    if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
+    __syncthreads();
+    {
+        int bad = 0;
+        if (t < 6) bad |= !isfinite(x0[t]);
+        if (t < 2) bad |= !isfinite(up[t]);
+        for (int i = t; i < 3 * (N + 1); i += NT) bad |= !isfinite(pref[i]);
+        for (int i = t; i < N + 1; i += NT) bad |= !isfinite(vr[i]);
+        if (bad) s_flag[0] = 1;
+    }
+
+    // ---- condensed QP (:180-250): P = sum_k F_k' F_k (+ the input penalties), q ----
+    // row r carries column r of the input sensitivity G_k; the free response xh is uniform.  Lane half h accumulates
+    // columns [h H, h H + H) of row r: Ph[i] = P_{r, h H + i}.
+    const double sw0 = sqrt(2.0 * c.q_c), sw1 = sqrt(2.0 * c.q_phi), sw2 = sqrt(2.0 * c.q_vx);
+    double xh[6], G[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 6; ++i) xh[i] = x0[i];
+    double qi = 0.0;
+    double Kh[H];   // row r, columns of half h: P during condensing and scaling, then K and K^-1
+#pragma unroll
+    for (int i = 0; i < H; ++i) Kh[i] = 0.0;
+    // A_k, B_k, g_k staged in LDS (coalesced copy) and read back as uniform broadcasts as the stage loop needs them:
+    // read from global memory the compiler issues all 54 loads of a stage at once, beside the 2H registers of Kh
+    for (int i = t; i < 36 * N; i += NT) s_lin[i] = gA[i];
+    for (int i = t; i < 12 * N; i += NT) s_lin[36 * N + i] = gB[i];
+    for (int i = t; i < 6 * N; i += NT) s_lin[48 * N + i] = gg[i];
+    __syncthreads();
+    for (int k = 0; k < N; ++k) {
+        const double* Ak = s_lin + 36 * k;
+        const double* Bk = s_lin + 36 * N + 12 * k;
+        const double* gk = s_lin + 48 * N + 6 * k;
+        double xn[6], Gn[6];
+        for (int rr = 0; rr < 6; ++rr) {
+            double v = gk[rr], w = 0.0;
+            for (int cc = 0; cc < 6; ++cc) {
+                v = fma(Ak[6 * rr + cc], xh[cc], v);
+                w = fma(Ak[6 * rr + cc], G[cc], w);
+            }
+            xn[rr] = v;
+            Gn[rr] = (own && kk == k) ? Bk[2 * rr + ch] : w;
+        }
+        for (int rr = 0; rr < 6; ++rr) { xh[rr] = xn[rr]; G[rr] = Gn[rr]; }
+        const int k1 = k + 1;
+        double sk, ck;
+        pm_sincos(pref[3 * k1 + 2], &sk, &ck);
+        const double e0 = sk * (xh[0] - pref[3 * k1]) - ck * (xh[1] - pref[3 * k1 + 1]);
+        const double e1 = xh[2] - pref[3 * k1 + 2];
+        const double e2 = xh[3] - vr[k1];
+        const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
+        qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
+        if (h == 0) { s_F[0][r] = F0; s_F[1][r] = F1; s_F[2][r] = F2; }
+        __syncthreads();
+        // F_k's columns >= 2 (k + 1) are zero (inputs of later stages; rows >= n hold F = 0): chunks of 8 columns from
+        // the first one that can be nonzero in half 0 (uniform skip); a half-1 lane's extra columns add exact zeros
+        const int jm = 2 * k + 2;
+        // (each chunk's 12 16-byte reads, then its 24 FMAs: the scheduler would otherwise issue every read first)
+        const double2* f2r[3] = {reinterpret_cast<const double2*>(&s_F[0][h * H]),
+                                 reinterpret_cast<const double2*>(&s_F[1][h * H]),
+                                 reinterpret_cast<const double2*>(&s_F[2][h * H])};
+#pragma unroll
+        for (int c0 = 0; c0 < H; c0 += 8) {
+            if (c0 >= jm) continue;
+            double2 f0[4], f1[4], f2[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                f0[i] = f2r[0][c0 / 2 + i];
+                f1[i] = f2r[1][c0 / 2 + i];
+                f2[i] = f2r[2][c0 / 2 + i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                Kh[c0 + 2 * i] = fma(F0, f0[i].x, fma(F1, f1[i].x, fma(F2, f2[i].x, Kh[c0 + 2 * i])));
+                Kh[c0 + 2 * i + 1] = fma(F0, f0[i].y, fma(F1, f1[i].y, fma(F2, f2[i].y, Kh[c0 + 2 * i + 1])));
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
+        }
+        __syncthreads();
+    }
+    // input penalties U'RU and dU'Rd dU (dU_0 = U_0 - u_prev): the band of row r
+    double Rs[4], Rds[4];
+    Rs[0] = c.R[0]; Rs[3] = c.R[3]; Rs[1] = Rs[2] = 0.5 * (c.R[1] + c.R[2]);
+    Rds[0] = c.Rd[0]; Rds[3] = c.Rd[3]; Rds[1] = Rds[2] = 0.5 * (c.Rd[1] + c.Rd[2]);
+    const double Rs0 = ch ? Rs[2] : Rs[0], Rs1 = ch ? Rs[3] : Rs[1];
+    const double Rd0 = ch ? Rds[2] : Rds[0], Rd1 = ch ? Rds[3] : Rds[1];
+    const double dmul = (kk < N - 1) ? 2.0 : 1.0;
+    if (own) {
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            const int j = h * H + i, kj = j >> 1;
+            const double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
+            double add = (kj == kk) ? 2.0 * rs + 2.0 * rd * dmul : 0.0;
+            add = (j < n && (kj == kk - 1 || kj == kk + 1)) ? -2.0 * rd : add;
+            Kh[i] = (j < n && (kj >= kk - 1 && kj <= kk + 1)) ? Kh[i] + add : Kh[i];
+        }
+        if (kk == 0) qi -= 2.0 * (Rd0 * up[0] + Rd1 * up[1]);
+    }
+    // row maximum |P_rj| (both halves)
+    auto row_absmax = [&]() -> double {
+        double m4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int i = 0; i < H; ++i) m4[i & 3] = vmax_abs(m4[i & 3], Kh[i]);
+        return pair_max(vmax(vmax(m4[0], m4[1]), vmax(m4[2], m4[3])));
+    };
+    // constraint rows owned by r: box (U_r) and rate (U_r - U_{r-2}, or U_0 - u_prev)
+    double lb = ch ? c.u_lo[1] : c.u_lo[0], ub = ch ? c.u_hi[1] : c.u_hi[0];
+    double lr = ch ? c.du_lo[1] : c.du_lo[0], ur = ch ? c.du_hi[1] : c.du_hi[0];
+    if (kk == 0) { lr += up[ch]; ur += up[ch]; }
+    const bool has_prev = kk > 0;
+    {
+        // (a NaN entry: the max propagates it; an infinite one is caught as non-finite)
+        const double am = row_absmax();
+        int bad = 0;
+        if (own) bad |= !isfinite(qi) || !isfinite(am);
+        if (bad) s_flag[0] = 1;
+    }
+    // exact feasibility of the box + rate chain (interval propagation)
+    if (t < 2) {
+        double lo = up[t], hi = up[t];
+        const double dlo = t ? c.du_lo[1] : c.du_lo[0], dhi = t ? c.du_hi[1] : c.du_hi[0];
+        const double ulo = t ? c.u_lo[1] : c.u_lo[0], uhi = t ? c.u_hi[1] : c.u_hi[0];
+        for (int k = 0; k < N; ++k) {
+            double nlo = lo + dlo, nhi = hi + dhi;
+            if (nlo < ulo) nlo = ulo;
+            if (nhi > uhi) nhi = uhi;
+            if (!(nlo <= nhi)) s_flag[1] = 1;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    __syncthreads();
+    const int early = s_flag[0] ? TRAJ_STATUS_SOLVER_ERROR : (s_flag[1] ? TRAJ_STATUS_INFEASIBLE : -1);
+    int status = TRAJ_STATUS_SOLVER_ERROR, iter = 0, pol = 0;
+    double xsol = 0.0;
+
+    if (early < 0) {
+        // ---- Ruiz equilibration + cost scaling (OSQP scale_data), as mpc_solve.h / mpc_long.h ----
+        double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0, cn = 0.0;
+        cn = own ? row_absmax() : 0.0;
+        for (int it = 0; it < c.scaling_iters; ++it) {
+            const double Er_up = exch(Er, +2), D_dn = exch(D, -2);
+            const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
+            const double pn = cs * cn;
+            const double coln = fmax(pn, fmax(fmax(fabs(a_b), fabs(a_r)), fabs(a_rp)));
+            const double Dt = own ? 1.0 / sqrt(limit_scaling(coln)) : 1.0;
+            const double Etb = 1.0 / sqrt(limit_scaling(fabs(a_b)));
+            const double Etr = 1.0 / sqrt(limit_scaling(fmax(fabs(a_r), fabs(a_rm))));
+            const double* dv = bcast(Dt);
+            double m4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int i = 0; i < H; ++i) {
+                const double w = Kh[i] * (Dt * dv[h * H + i]);
+                Kh[i] = w;
+                m4[i & 3] = vmax_abs(m4[i & 3], w);
+            }
+            cn = own ? pair_max(vmax(vmax(m4[0], m4[1]), vmax(m4[2], m4[3]))) : 0.0;
+            qi *= Dt;
+            D *= Dt;
+            Eb *= Etb;
+            Er *= Etr;
+            const double mean = block_sum(own ? cs * cn : 0.0) / n;
+            double qv[1] = {own ? fabs(cs * qi) : 0.0};
+            block_max(qv);
+            double ct = fmax(mean, limit_scaling(qv[0]));
+            ct = 1.0 / limit_scaling(ct);
+            cs *= ct;
+        }
+#pragma unroll
+        for (int i = 0; i < H; ++i) Kh[i] *= cs;
+        qi *= cs;
+        // the scaled P to the scratch (row r's half h at Pg + r PL + h H); the padding rows r >= n hold the identity
+        // row there (zero otherwise), so that K's padding pivots are trivial
+        if (r < NR) {
+            double2* w2 = reinterpret_cast<double2*>(Pg + (size_t)r * PL + h * H);
+#pragma unroll
+            for (int i = 0; i < H; i += 2) w2[i / 2] = double2{Kh[i], Kh[i + 1]};
+            if (!own && h == r / H) Pg[(size_t)r * PL + r] = 1.0;
+        }
+        const double csinv = 1.0 / cs;
+        const double D_dn = exch(D, -2);
+        const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0;
+        const double a_r_up = exch(a_r, +2);
+        const double slb = (lb > -INFTY) ? lb * Eb : -INFTY, sub = (ub < INFTY) ? ub * Eb : INFTY;
+        const double slr = (lr > -INFTY) ? lr * Er : -INFTY, sur = (ur < INFTY) ? ur * Er : INFTY;
+        const double Dinv = 1.0 / D, Ebinv = 1.0 / Eb, Erinv = 1.0 / Er;
+        __syncthreads();   // P in the scratch (read back by other lanes' row loads only through the same lane: no hazard)
+
+        // ---- helpers over the scaled problem ----
+        auto Ax = [&](double v, double& zb, double& zr) {
+            const double vdn = exch(v, -2);
+            zb = a_b * v;
+            zr = a_r * v - a_rm * vdn;
+        };
+        auto ATw = [&](double wb, double wr) -> double {
+            const double rp_up = exch(a_rm * wr, +2);   // a_rp(r) wr(r+2), formed on row r+2
+            return a_b * wb + a_r * wr - rp_up;
+        };
+        // (P v)_r: the half-row from the scratch (16-byte loads, all in flight), 4 chains, the pair sum
+        auto Pmul = [&](double v) -> double {
+            const double* vb = bcast(v);
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+            const double2* p2 = reinterpret_cast<const double2*>(Pg + (size_t)(r < NR ? r : NR - 1) * PL + h * H);
+#pragma unroll
+            for (int i0 = 0; i0 < H; i0 += 16) {
+                double2 pv[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) pv[i] = p2[i0 / 2 + i];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    s4[(2 * i) & 3] = fma(pv[i].x, vb[h * H + i0 + 2 * i], s4[(2 * i) & 3]);
+                    s4[(2 * i + 1) & 3] = fma(pv[i].y, vb[h * H + i0 + 2 * i + 1], s4[(2 * i + 1) & 3]);
+                }
+            }
+            const double s = pair_sum((s4[0] + s4[1]) + (s4[2] + s4[3]));
+            return own ? s : 0.0;
+        };
+        // (K^-1 v)_r from the register half-rows: the broadcast half in chunks of 8 (16-byte reads), 4 chains
+        auto Kmul = [&](double v) -> double {
+            const double* vb = bcast(v);
+            const double2* v2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb + h * H, 16));
+            double s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int i0 = 0; i0 < H; i0 += 8) {
+                double2 vv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) vv[i] = v2[i0 / 2 + i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    s4[(i0 + 2 * i) & 3] = fma(Kh[i0 + 2 * i], vv[i].x, s4[(i0 + 2 * i) & 3]);
+                    s4[(i0 + 2 * i + 1) & 3] = fma(Kh[i0 + 2 * i + 1], vv[i].y, s4[(i0 + 2 * i + 1) & 3]);
+                }
+            }
+            const double s = pair_sum((s4[0] + s4[1]) + (s4[2] + s4[3]));
+            return own ? s : 0.0;
+        };
+        auto rho_for = [&](double l, double u, double rho) -> double {
+            if (l <= -INFTY * MIN_SCALING && u >= INFTY * MIN_SCALING) return RHO_MIN;
+            if (u - l < RHO_TOL) return RHO_EQ_OVER_INEQ * rho;
+            return rho;
+        };
+        struct Res { double pr, dr, eps_p, eps_d, prs, drs, pn, dn; };
+        auto residuals = [&](double x, double zb, double zr, double yb, double yr) -> Res {
+            const double px = Pmul(x);
+            double axb, axr;
+            Ax(x, axb, axr);
+            const double aty = ATw(yb, yr);
+            double v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (own) {
+                const double dres = px + qi + aty;
+                v[0] = fmax(fabs(Ebinv * (axb - zb)), fabs(Erinv * (axr - zr)));
+                v[1] = fmax(fmax(fabs(Ebinv * axb), fabs(Erinv * axr)), fmax(fabs(Ebinv * zb), fabs(Erinv * zr)));
+                v[2] = fabs(Dinv * dres) * csinv;
+                v[3] = fmax(fabs(Dinv * px) * csinv, fmax(fabs(Dinv * aty) * csinv, fabs(Dinv * qi) * csinv));
+                v[4] = fmax(fabs(axb - zb), fabs(axr - zr));
+                v[5] = fabs(dres);
+                v[6] = fmax(fmax(fabs(axb), fabs(axr)), fmax(fabs(zb), fabs(zr)));
+                v[7] = fmax(fmax(fabs(aty), fabs(qi)), fabs(px));
+            }
+            block_max(v);
+            Res rs;
+            rs.pr = v[0]; rs.eps_p = c.eps_abs + c.eps_rel * v[1];
+            rs.dr = v[2]; rs.eps_d = c.eps_abs + c.eps_rel * v[3];
+            rs.prs = v[4]; rs.drs = v[5]; rs.pn = v[6]; rs.dn = v[7];
+            return rs;
+        };
+
+        // ---- ADMM (osqp_solve) + polish around one factorization site ----
+        constexpr int PH_ADMM = 0, PH_POLISH = 1, PH_DONE = 2;
+        int phase = PH_ADMM;
+        double rho = c.rho;
+        if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {   // closed-loop warm start: the previous step's rho
+            const double* wv = a.wsWarm + 4 * (size_t)b;
+            if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
+        }
+        double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
+        double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
+        Res rs0 = {0, 0, 0, 0, 0, 0, 0, 0};
+        int rounds = 0, ps = 0, actb = 0, actr = 0;
+        double escale = 1.0;
+        const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
+        iter = 1;
+        while (phase != PH_DONE) {
+            // ---- K = P + ks I + A' diag(kb, kr) A (row r, half h from the scratch), then the sweep: K <- -K^-1 ----
+            const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
+            const double kr = (phase == PH_ADMM) ? rr : (actr ? 1.0 / dl : 0.0);
+            const double ks = (phase == PH_ADMM) ? sig : dl;
+            {
+                const double kr_up = exch(kr, +2);
+                const double a_rp = exch(a_rm, +2);   // Er(r+2) D(r)
+                const double dii = ks + kb * a_b * a_b + kr * a_r * a_r + kr_up * a_rp * a_rp;
+                const double dp = -kr_up * a_r_up * a_rp;          // (r, r+2)
+                const double dm = -kr * a_r * a_rm;                // (r, r-2): row r-2's dp, the same product
+                // The band goes into P in the scratch (row r's half-0 lane adds its diagonal and its (r, r +- 2) entries),
+                // both lanes load the row half as it stands -- no per-entry selects (their masks, invariant across the
+                // solve, are what the compiler would hoist and spill) -- and the three entries are restored.
+                double* const prow = Pg + (size_t)(r < NR ? r : NR - 1) * PL;
+                double o_dg = 0.0, o_sp = 0.0, o_sm = 0.0;
+                const bool has_sp = own && r + 2 < n, has_sm = own && has_prev;
+                if (own && h == 0) {
+                    o_dg = prow[r];
+                    prow[r] = o_dg + dii;
+                    if (has_sp) { o_sp = prow[r + 2]; prow[r + 2] = o_sp + dp; }
+                    if (has_sm) { o_sm = prow[r - 2]; prow[r - 2] = o_sm + dm; }
+                }
+                __syncthreads();
+                const double2* p2 = reinterpret_cast<const double2*>(prow + h * H);
+#pragma unroll
+                for (int i = 0; i < H; i += 2) {
+                    const double2 pv = p2[i / 2];
+                    Kh[i] = pv.x;
+                    Kh[i + 1] = pv.y;
+                }
+                __syncthreads();
+                if (own && h == 0) {
+                    prow[r] = o_dg;
+                    if (has_sp) prow[r + 2] = o_sp;
+                    if (has_sm) prow[r - 2] = o_sm;
+                }
+            }
+            // The sweep: pivot p in half hp = p / H, q = p mod H.  Before pivot p both halves are rotated by q: register
+            // i of half h holds column h H + (i + q) mod H, so column p is register 0 of half hp.  The pivot column
+            // (= the pivot row, K symmetric) is published as two contiguous rotated slices per half, so each lane reads
+            // its rotated pivot-row entries from one 16-byte aligned slice.  Pivots past n (padding) only rotate.
+            bool ok = true;
+            for (int hp = 0; hp < 2; ++hp) {
+#pragma unroll 2
+                for (int q = 0; q < H; ++q) {
+                    const int pv = hp * H + q;
+                    if (pv >= n) {   // padding pivot: the identity row, a rotation only
+                        const double k0 = Kh[0];
+#pragma unroll
+                        for (int i = 1; i < H; ++i) Kh[i - 1] = Kh[i];
+                        Kh[H - 1] = k0;
+                        continue;
+                    }
+                    double e0, e1;
+                    swap32(Kh[0], e0, e1);
+                    const double kp = hp ? e1 : e0;            // K[r][p]: register 0 of the half holding column p
+                    const int par = pv & 1, off = q & 1;
+                    double* const sl = &s_pv[par][0][0];
+                    // row r publishes its K[r][p] = K[p][r] at slice position (r mod H) and (r mod H) + H of half r / H
+                    if (r < NR) sl[(r / H) * SPV + off + (r % H) + h * H] = kp;
+                    __syncthreads();
+                    const double d = sl[hp * SPV + off + q];
+                    ok = ok && (d > 0.0);
+                    const double dinv = rcp_nr(d);
+                    const bool piv = (r == pv);
+                    const double fd = kp * dinv;
+                    const double be = piv ? dinv : -fd;
+                    const double k0 = piv ? -dinv : fd;
+                    if (piv) {   // the pivot row becomes K_pj / d: an exact zero row plus be * K_pj
+#pragma unroll
+                        for (int i = 0; i < H; ++i) Kh[i] = 0.0;
+                    }
+                    // rotated pivot-row entries of this half: K[p][h H + (i + q) mod H] at sl[h SPV + off + q + i]
+                    const double2* pr2 =
+                        reinterpret_cast<const double2*>(__builtin_assume_aligned(sl + h * SPV + off + q, 16));
+                    double2 cur[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cur[i] = pr2[i];
+                    const double last = fma3(be, cur[0].x, Kh[0]);   // column h H + q (the non-pivot half's entry)
+#pragma unroll
+                    for (int i0 = 0; i0 < H; i0 += 8) {
+                        double2 nxt[4];
+                        if (i0 + 8 < H) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) nxt[i] = pr2[(i0 + 8) / 2 + i];
+                        }
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int j = i0 + 2 * i;
+                            // (three-address fma: the rotated destination is written directly, no register copies)
+                            if (j > 0) Kh[j - 1] = fma3(be, cur[i].x, Kh[j]);
+                            Kh[j] = fma3(be, cur[i].y, Kh[j + 1]);
+                        }
+                        if (i0 + 8 < H) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) cur[i] = nxt[i];
+                        }
+                    }
+                    Kh[H - 1] = (h == hp) ? k0 : last;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < H; ++i) Kh[i] = -Kh[i];
+            __syncthreads();
+            if (!ok) {
+                if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
+                if (c.polish_mode == 1 && rounds < c.polish_max_rounds && iter < c.max_iter) {
+                    ++rounds;
+                    escale *= 1e-2;
+                    ++iter;
+                    phase = PH_ADMM;
+                } else {
+                    phase = PH_DONE;
+                }
+                continue;
+            }
+            if (phase == PH_ADMM) {
+                bool converged = false, refactor = false;
+                int chk = c.check_interval - (iter - 1) % c.check_interval;
+                const double oma = 1.0 - alpha;
+                const double rib = 1.0 / rb, rir = 1.0 / rr;
+                for (; iter <= c.max_iter; ++iter) {
+                    const double wb = fma(rb, zb, -yb), wr = fma(rr, zr, -yr);
+                    const double rp_up = exch(a_rm * wr, +2);
+                    const double atw = fma(a_b, wb, fma(a_r, wr, -rp_up));
+                    const double xt = Kmul(fma(sig, x, atw - qi));
+                    const double xt_dn = exch(xt, -2);
+                    const double ztb = a_b * xt, ztr = fma(a_r, xt, -(a_rm * xt_dn));
+                    const double xn = fma(alpha, xt, oma * x);
+                    const double zrb = fma(alpha, ztb, oma * zb), zrr = fma(alpha, ztr, oma * zr);
+                    const double nzb = clamp_mm(fma(rib, yb, zrb), slb, sub), nzr = clamp_mm(fma(rir, yr, zrr), slr, sur);
+                    yb = fma(rb, zrb - nzb, yb);
+                    yr = fma(rr, zrr - nzr, yr);
+                    x = xn;
+                    zb = nzb;
+                    zr = nzr;
+                    if (--chk == 0) {
+                        chk = c.check_interval;
+                        rs0 = residuals(x, zb, zr, yb, yr);
+                        if (rs0.pr <= escale * rs0.eps_p && rs0.dr <= escale * rs0.eps_d) { converged = true; break; }
+                        if (c.adaptive_rho) {
+                            double est = rho * sqrt((rs0.prs / (rs0.pn + DIV_TOL)) / (rs0.drs / (rs0.dn + DIV_TOL) + DIV_TOL));
+                            est = fmin(fmax(est, RHO_MIN), RHO_MAX);
+                            if (est > rho * c.adaptive_rho_tol || est < rho / c.adaptive_rho_tol) {
+                                rho = est;
+                                rb = rho_for(slb, sub, rho);
+                                rr = rho_for(slr, sur, rho);
+                                refactor = true;
+                                ++iter;
+                                break;
+                            }
+                        }
+                    }
+                }
+                if (refactor && iter <= c.max_iter) continue;
+                if (converged) status = TRAJ_STATUS_OPTIMAL;
+                else {
+                    iter = c.max_iter;
+                    rs0 = residuals(x, zb, zr, yb, yr);
+                    status = (rounds > 0 && rs0.pr <= rs0.eps_p && rs0.dr <= rs0.eps_d) ? TRAJ_STATUS_OPTIMAL
+                             : (rs0.pr <= 10.0 * rs0.eps_p && rs0.dr <= 10.0 * rs0.eps_d) ? TRAJ_STATUS_OPTIMAL_INACCURATE
+                                                                                       : TRAJ_STATUS_USER_LIMIT;
+                }
+                if (status == TRAJ_STATUS_OPTIMAL && c.polish) {
+                    // OSQP active sets: lower if z - l < -y, upper if u - z < y
+                    actb = own ? ((zb - slb < -yb) ? -1 : ((sub - zb < yb) ? 1 : 0)) : 0;
+                    actr = own ? ((zr - slr < -yr) ? -1 : ((sur - zr < yr) ? 1 : 0)) : 0;
+                    ps = 1;
+                    phase = PH_POLISH;
+                } else {
+                    phase = PH_DONE;
+                }
+                continue;
+            }
+            // ---- polish: K^-1 = M^-1, M = P + delta I + Ar' Ar / delta (the eliminated reduced KKT) ----
+            {
+                const double bbv = actb < 0 ? slb : (actb > 0 ? sub : 0.0);
+                const double brv = actr < 0 ? slr : (actr > 0 ? sur : 0.0);
+                double px_ = 0.0, pyb = 0.0, pyr = 0.0;
+                double r1 = -qi, r2b = actb ? bbv : 0.0, r2r = actr ? brv : 0.0;
+                double axb = 0.0, axr = 0.0;
+                for (int rf = 0; rf <= c.polish_refine_iter; ++rf) {
+                    const double tv = Kmul(r1 + ATw(actb ? r2b / dl : 0.0, actr ? r2r / dl : 0.0));
+                    double tb, tr;
+                    Ax(tv, tb, tr);
+                    px_ += tv;
+                    if (actb) pyb += (tb - r2b) / dl;
+                    if (actr) pyr += (tr - r2r) / dl;
+                    if (rf == c.polish_refine_iter) break;
+                    const double Pxv = Pmul(px_);
+                    const double atyv = ATw(pyb, pyr);
+                    r1 = -qi - Pxv - atyv;
+                    Ax(px_, axb, axr);
+                    r2b = actb ? bbv - axb : 0.0;
+                    r2r = actr ? brv - axr : 0.0;
+                }
+                Ax(px_, axb, axr);
+                if (c.polish_mode == 0) {
+                    // z = proj(Ax + y), y = Ax + y - z (OSQP project_normalcone); accept if the residuals drop
+                    const double ztb = axb + pyb, ztr = axr + pyr;
+                    const double nzb = clampd(ztb, slb, sub), nzr = clampd(ztr, slr, sur);
+                    const double nyb = ztb - nzb, nyr = ztr - nzr;
+                    const Res rp = residuals(px_, nzb, nzr, nyb, nyr);
+                    const bool okp = (rp.pr < rs0.pr && rp.dr < rs0.dr) || (rp.pr < rs0.pr && rs0.dr < 1e-10) ||
+                                     (rp.dr < rs0.dr && rs0.pr < 1e-10);
+                    if (okp) {
+                        x = px_; zb = nzb; zr = nzr; yb = nyb; yr = nyr;
+                        pol = 1;
+                    }
+                    phase = PH_DONE;
+                    continue;
+                }
+                // exact mode: the KKT certificate in the unscaled problem
+                const double Pxv = Pmul(px_);
+                const double atyv = ATw(pyb, pyr);
+                const double tol = c.cert_tol;
+                double v[2];
+                double lb_ = ch ? c.u_lo[1] : c.u_lo[0], ub_ = ch ? c.u_hi[1] : c.u_hi[0];
+                double lr_ = ch ? c.du_lo[1] : c.du_lo[0], ur_ = ch ? c.du_hi[1] : c.du_hi[0];
+                if (kk == 0) { lr_ += up[ch]; ur_ += up[ch]; }
+                v[0] = own ? fabs(Dinv * (Pxv + qi + atyv)) * csinv : 0.0;            // stationarity
+                v[1] = own ? fmax(fabs(Dinv * qi), fabs(Dinv * Pxv)) * csinv : 0.0;  // gradient scale
+                block_max(v);
+                const double gsc = fmax(1.0, v[1]);
+                int okc = v[0] <= tol * gsc;
+                if (own) {
+                    const double axu = axb * Ebinv, arv = axr * Erinv;
+                    if (slb > -INFTY && axu < lb_ - tol * (1.0 + fabs(lb_))) okc = 0;
+                    if (sub < INFTY && axu > ub_ + tol * (1.0 + fabs(ub_))) okc = 0;
+                    if (slr > -INFTY && arv < lr_ - tol * (1.0 + fabs(lr_))) okc = 0;
+                    if (sur < INFTY && arv > ur_ + tol * (1.0 + fabs(ur_))) okc = 0;
+                    const double ybu = pyb * Eb * csinv, yru = pyr * Er * csinv;
+                    if (actb < 0 && ybu > tol * gsc) okc = 0;
+                    if (actb > 0 && ybu < -tol * gsc) okc = 0;
+                    if (actr < 0 && yru > tol * gsc) okc = 0;
+                    if (actr > 0 && yru < -tol * gsc) okc = 0;
+                }
+                double fo[1] = {okc ? 0.0 : 1.0};
+                block_max(fo);
+                if (fo[0] == 0.0) {
+                    x = px_;
+                    zb = clampd(axb, slb, sub);
+                    zr = clampd(axr, slr, sur);
+                    yb = pyb;
+                    yr = pyr;
+                    pol = ps + 16 * rounds;
+                    phase = PH_DONE;
+                    continue;
+                }
+                if (ps < c.polish_max_pass) {
+                    // primal-dual active-set update with the OSQP rule on the polished (Ax, y)
+                    actb = own ? ((axb - slb < -pyb) ? -1 : ((sub - axb < pyb) ? 1 : 0)) : 0;
+                    actr = own ? ((axr - slr < -pyr) ? -1 : ((sur - axr < pyr) ? 1 : 0)) : 0;
+                    ++ps;
+                    continue;
+                }
+                if (rounds < c.polish_max_rounds && iter < c.max_iter) {
+                    // not certified: continue ADMM to a 100x tighter tolerance, then polish again
+                    ++rounds;
+                    escale *= 1e-2;
+                    ++iter;
+                    phase = PH_ADMM;
+                    continue;
+                }
+                phase = PH_DONE;
+            }
+        }
+        if (iter > c.max_iter) iter = c.max_iter;
+        xsol = D * x;
+        if (CLOSED && a.wsWarm && t == 0) {
+            double* wv = a.wsWarm + 4 * (size_t)b;
+            wv[0] = rho;
+            wv[1] = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE) ? 1.0 : 0.0;
+            wv[2] = (double)iter;
+        }
+    } else {
+        status = early;
+        iter = 0;
+        if (CLOSED && a.wsWarm && t == 0) {
+            a.wsWarm[4 * (size_t)b + 1] = 0.0;
+            a.wsWarm[4 * (size_t)b + 2] = 0.0;
+        }
+    }
+
+    // ---- outputs (:257-275): U, X_opt by the linear model, the objective, u_cmd (CLOSED: the plant update) ----
+    const bool good = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE);
+    const double nan = __builtin_nan("");
+    double* const Ub = s_bc[0];
+    __syncthreads();
+    if (h == 0) Ub[r] = own ? xsol : 0.0;
+    __syncthreads();
+    if constexpr (CLOSED) {
+        // plant x <- x + Ts f(x, u_cmd) (main.py:97), u_prev <- u_cmd (:101); the history and this step's outcome
+        if (t == 0) {
+            const double uc0 = good ? Ub[0] : up[0], uc1 = good ? Ub[1] : up[1];
+            double xs[6], f[6], u[2] = {uc0, uc1};
+            for (int i = 0; i < 6; ++i) xs[i] = x0[i];
+            f_cont(p, xs, u, f);
+            for (int i = 0; i < 6; ++i) {
+                const double xn = xs[i] + c.Ts * f[i];
+                a.x_state[6 * (size_t)b + i] = xn;
+                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + a.t + 1) * 6 + i] = xn;
+            }
+            a.u_state[2 * (size_t)b] = uc0;
+            a.u_state[2 * (size_t)b + 1] = uc1;
+            if (a.hist_u) {
+                a.hist_u[((size_t)b * a.hist_T + a.t) * 2] = uc0;
+                a.hist_u[((size_t)b * a.hist_T + a.t) * 2 + 1] = uc1;
+            }
+            if (a.status) a.status[b] = status;
+            if (a.iters) a.iters[b] = iter;
+        }
+        return;
+    }
+    // X_{k+1} = A_k X_k + B_k U_k + g_k, stage by stage (thread i < 6: state i)
+    double* const Xs = s_xs;
+    if (t < 6) Xs[t] = x0[t];
+    __syncthreads();
+    for (int k = 0; k < N; ++k) {
+        if (t < 6) {
+            double v = 0.0;
+            for (int cc = 0; cc < 6; ++cc) v += gA[k * 36 + t * 6 + cc] * Xs[6 * k + cc];
+            v += gB[k * 12 + t * 2] * Ub[2 * k] + gB[k * 12 + t * 2 + 1] * Ub[2 * k + 1] + gg[6 * k + t];
+            Xs[6 * (k + 1) + t] = v;
+        }
+        __syncthreads();
+    }
+    // objective: the cost of :217-250 at (X_opt, U_opt), k = t over the threads, summed in a fixed order
+    double op = 0.0;
+    for (int k = t; k <= N; k += NT) {
+        const double* X = Xs + 6 * k;
+        double s, co;
+        pm_sincos(pref[3 * k + 2], &s, &co);
+        const double ec = s * (X[0] - pref[3 * k]) - co * (X[1] - pref[3 * k + 1]);
+        const double ep = X[2] - pref[3 * k + 2];
+        const double ev = X[3] - vr[k];
+        op += c.q_c * ec * ec + c.q_phi * ep * ep + c.q_vx * ev * ev;
+        if (k < N) {
+            const double u0 = Ub[2 * k], u1 = Ub[2 * k + 1];
+            const double d0 = u0 - (k == 0 ? up[0] : Ub[2 * k - 2]);
+            const double d1 = u1 - (k == 0 ? up[1] : Ub[2 * k - 1]);
+            op += u0 * (c.R[0] * u0 + c.R[1] * u1) + u1 * (c.R[2] * u0 + c.R[3] * u1);
+            op += d0 * (c.Rd[0] * d0 + c.Rd[1] * d1) + d1 * (c.Rd[2] * d0 + c.Rd[3] * d1);
+        }
+    }
+    // (every thread's partial -- not only half 0's rows: block_sum takes half-0 lanes, so sum by thread here)
+    op = wave_sum_dpp(op);
+    if (lane == 0) s_red[wid * 8] = op;
+    __syncthreads();
+    double obj = 0.0;
+    for (int w = 0; w < WAVES; ++w) obj += s_red[w * 8];
+    if (t == 0) {
+        a.u_cmd[2 * b] = good ? Ub[0] : up[0];
+        a.u_cmd[2 * b + 1] = good ? Ub[1] : up[1];
+        a.status[b] = status;
+        if (a.objective) a.objective[b] = good ? obj : nan;
+        if (a.iters) a.iters[b] = iter;
+        if (a.polished) a.polished[b] = pol;
+    }
+    if (a.U_opt && own && h == 0) a.U_opt[(size_t)b * 2 * N + ch * N + kk] = good ? xsol : nan;
+    if (a.X_opt)
+        for (int i = t; i < 6 * (N + 1); i += NT) {
+            const int rr = i / (N + 1), k = i % (N + 1);
+            a.X_opt[(size_t)b * 6 * (N + 1) + i] = good ? Xs[6 * k + rr] : nan;
+        }
+}
+
+}  // namespace tgmpc

@@ -239,7 +239,9 @@ static int launch_general(const KArgs& a, double* gws, hipStream_t st) {
 }
 
 // the long-horizon kernel (mpc_long.h): TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG without state bounds; its per-instance
-// scratch (the scaled P, and K^-1 past LONG_NKL) is the caller's, in the same region as the general solver's
+// scratch (the scaled P, and K^-1 past LONG_NKL) is the caller's, in the same region as the general solver's.
+// CLOSED: one closed-loop step (window from the state, warm rho, plant update) -- traj_closed_loop_step / _run.
+template <bool CLOSED>
 static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
     const int N = a.c.N;
     const size_t per = long_ws_doubles(N);
@@ -251,17 +253,26 @@ static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
         int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return TRAJ_E_LAUNCH;
         if (dev < 0 || dev >= 64 || !attr[dev].load(std::memory_order_acquire)) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_long_kernel<true>),
+            if (hipFuncSetAttribute(reinterpret_cast<const void*>(&solve_long_kernel<true, CLOSED>),
                                     hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)(LONG_NKL * LONG_NKL * sizeof(double))) != hipSuccess)
                 return TRAJ_E_LAUNCH;
             if (dev >= 0 && dev < 64) attr[dev].store(true, std::memory_order_release);
         }
-        hipLaunchKernelGGL(solve_long_kernel<true>, dim3(a.B), dim3(LONG_NT), lds, st, a, lws, per);
+        hipLaunchKernelGGL((solve_long_kernel<true, CLOSED>), dim3(a.B), dim3(LONG_NT), lds, st, a, lws, per);
     } else {
-        hipLaunchKernelGGL(solve_long_kernel<false>, dim3(a.B), dim3(LONG_NT), 0, st, a, lws, per);
+        hipLaunchKernelGGL((solve_long_kernel<false, CLOSED>), dim3(a.B), dim3(LONG_NT), 0, st, a, lws, per);
     }
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+// the row-split kernel (mpc_split.h; split_inst.hip, its own translation unit built without machine LICM like the
+// other register-resident solvers): TRAJ_MAX_N < N <= TRAJ_MAX_N_SPLIT without state bounds
+int launch_split_step(const KArgs& a, double* sws, hipStream_t st);
+int launch_split_closed(const KArgs& a, double* sws, hipStream_t st);
+template <bool CLOSED>
+static int launch_split(const KArgs& a, double* sws, hipStream_t st) {
+    return CLOSED ? launch_split_closed(a, sws, st) : launch_split_step(a, sws, st);
 }
 
 // fused run queue order: the heaviest 10 % of the instances (by the previous launch's mean ADMM
@@ -296,6 +307,9 @@ static int g_lead_steps = TGMPC_LEAD_STEPS, g_lead_permille = TGMPC_LEAD_PERMILL
 #define TGMPC_RUN_AHEAD 0
 #endif
 static int g_run_ahead = TGMPC_RUN_AHEAD;   // traj_debug_run_ahead
+// horizons up to which TRAJ_MAX_N < N runs the row-split kernel (mpc_split.h) instead of the long-horizon one
+// (traj_debug_split_max_n: 0 sends every N > TRAJ_MAX_N to the long-horizon kernel; the two agree to the step bars)
+static int g_split_max_n = TRAJ_MAX_N_SPLIT;
 // traj_debug_step_linearize: the step's linearization inside the solve launch.  An atomic: a test that flips it may run
 // beside other callers of the library; each traj_mpc_step_batch reads it once.
 static std::atomic<int> g_step_inlin{1};
@@ -350,6 +364,12 @@ int traj_debug_queue_lead(int steps, int per_mille) {
 int traj_debug_run_ahead(int levels) {
     if (levels < 0) return TRAJ_E_ARG;
     g_run_ahead = levels;
+    return TRAJ_OK;
+}
+
+int traj_debug_split_max_n(int n_max) {
+    if (n_max < 0 || n_max > TRAJ_MAX_N_SPLIT) return TRAJ_E_ARG;
+    g_split_max_n = n_max;
     return TRAJ_OK;
 }
 
@@ -532,7 +552,8 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (lin && (sb || !inlin)) launch_linearize(a, (hipStream_t)stream, false);
     if (sb) {
         double* const sws = (double*)((char*)ws + base);
-        if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long(a, sws, (hipStream_t)stream);
+        if (!state_bounds_active(c) && c->N <= g_split_max_n) return launch_split<false>(a, sws, (hipStream_t)stream);
+        if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long<false>(a, sws, (hipStream_t)stream);
         return launch_general(a, sws, (hipStream_t)stream);
     }
     return launch_mpc(a, (hipStream_t)stream, lin ? (inlin ? 4 : 0) : 1);
@@ -587,16 +608,45 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
+// The closed loop's horizons: N <= TRAJ_MAX_N on the register-resident kernels (fused or per step), TRAJ_MAX_N < N <=
+// TRAJ_MAX_N_LONG on the long-horizon kernel, one step per launch sequence (rollout_kernel + jac_kernel + the closed
+// solve_long_kernel); no state bounds (main.py passes none).  The long tier needs the step's scratch beside the
+// workspace, as the step entry point does: traj_mpc_workspace_bytes + traj_mpc_sb_workspace_bytes.
+static int check_cfg_closed(const traj_mpc_config* c) {
+    if (c && c->N > TRAJ_MAX_N && c->N <= TRAJ_MAX_N_LONG) {
+        const int e = check_cfg(c, true);
+        if (e) return e;
+        return state_bounds_active(c) ? TRAJ_E_UNSUPPORTED : TRAJ_OK;
+    }
+    return check_cfg(c);
+}
+static size_t closed_ws_bytes(int B, int N) {
+    return traj_mpc_workspace_bytes(B, N) + (N > TRAJ_MAX_N ? traj_mpc_sb_workspace_bytes(B, N) : 0);
+}
+// one long-horizon closed-loop step on a's state (a.t = the step, a.status / a.iters = this step's [B] rows)
+static int closed_step_long(const KArgs& a, void* ws, hipStream_t st) {
+    stamp(0, st);
+    launch_linearize(a, st, true);
+    stamp(1, st);
+    stamp(2, st);
+    stamp(3, st);
+    double* const sws = (double*)((char*)ws + ws_base_bytes(a.B, a.c.N));
+    const int e = (a.c.N <= g_split_max_n) ? launch_split<true>(a, sws, st) : launch_long<true>(a, sws, st);
+    stamp(4, st);
+    if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
+    return e;
+}
+
 int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
                           double* x, double* u_prev, const double* vref, int t, int hist_T, double* hist_x,
                           double* hist_u, int* status, int* iters, void* workspace, size_t workspace_bytes,
                           void* stream) {
     if (!p || B < 0 || !paths_ok(paths)) return TRAJ_E_ARG;
-    int e = check_cfg(c);
+    int e = check_cfg_closed(c);
     if (e) return e;
     if (B == 0) return TRAJ_OK;
     if (!x || !u_prev || !vref) return TRAJ_E_ARG;
-    if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, c->N)) return TRAJ_E_ARG;
+    if (!workspace || workspace_bytes < closed_ws_bytes(B, c->N)) return TRAJ_E_ARG;
     if ((hist_x || hist_u) && (t < 0 || t >= hist_T)) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -616,6 +666,7 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.dbg = g_dbg;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
+    if (c->N > TRAJ_MAX_N) return closed_step_long(a, workspace, st);
     const int nr = (B + 63) / 64, nj = (B * c->N + 63) / 64;
     stamp(0, st);
     hipLaunchKernelGGL(rollout_kernel<true>, dim3(nr), dim3(64), 0, st, a);
@@ -640,11 +691,11 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
                          double* hist_x, double* hist_u, int* status, int* iters, void* workspace,
                          size_t workspace_bytes, void* stream) {
     if (!p || B < 0 || steps < 0 || !paths_ok(paths)) return TRAJ_E_ARG;
-    int e = check_cfg(c);
+    int e = check_cfg_closed(c);
     if (e) return e;
     if (B == 0 || steps == 0) return TRAJ_OK;
     if (!x || !u_prev || !vref || t0 < 0) return TRAJ_E_ARG;
-    if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, c->N)) return TRAJ_E_ARG;
+    if (!workspace || workspace_bytes < closed_ws_bytes(B, c->N)) return TRAJ_E_ARG;
     if ((hist_x || hist_u) && t0 + steps > hist_T) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -679,6 +730,21 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.queue = (int*)(a.wsWarm + (size_t)B * 4) + B;
     if (hipMemsetAsync(a.queue, 0, ((size_t)B * 2 + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
     a.run_ahead = g_run_ahead;
+    if (c->N > TRAJ_MAX_N) {
+        // past the register-resident capacity: the steps as long-horizon step launch sequences, in order on the stream
+        // (the same results as that many traj_closed_loop_step calls; the queue above stays clear, so
+        // traj_closed_loop_check reports TRAJ_OK)
+        for (int s = 0; s < steps; ++s) {
+            KArgs as = a;
+            as.t = t0 + s;
+            as.status = status ? status + (size_t)s * B : nullptr;
+            as.iters = iters ? iters + (size_t)s * B : nullptr;
+            as.nsteps = 0;
+            e = closed_step_long(as, workspace, st);
+            if (e) return e;
+        }
+        return TRAJ_OK;
+    }
     stamp(0, st);
     stamp(1, st);
     stamp(2, st);
@@ -714,7 +780,7 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
 }
 
 int traj_closed_loop_check(const void* workspace, size_t workspace_bytes, int B, int N, void* stream) {
-    if (B < 0 || N < 1 || N > TRAJ_MAX_N) return TRAJ_E_ARG;
+    if (B < 0 || N < 1 || N > TRAJ_MAX_N_LONG) return TRAJ_E_ARG;
     if (B == 0) return TRAJ_OK;
     if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, N)) return TRAJ_E_ARG;
     KArgs a;
