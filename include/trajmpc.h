@@ -280,6 +280,10 @@ int traj_debug_step_linearize(int in_kernel);
  * long-horizon kernel (0: every N > TRAJ_MAX_N on the long-horizon kernel).  Both restate the same solver; for the
  * tests that compare them.  Diagnostics only. */
 int traj_debug_split_max_n(int n_max);
+/* Horizons n_min <= N <= TRAJ_MAX_N also run the row-split kernel on the step and per-step closed-loop paths (21 ..
+ * TRAJ_MAX_N + 1; default TRAJ_MAX_N + 1 = none; the scratch of traj_mpc_sb_workspace_bytes is then needed as past
+ * TRAJ_MAX_N).  For the experiments that compare it with the capacity-80 kernel.  Diagnostics only. */
+int traj_debug_split_min_n(int n_min);
 
 #ifdef __cplusplus
 }

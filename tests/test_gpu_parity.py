@@ -1055,3 +1055,82 @@ def test_closed_loop_long_horizon_per_step(gpu, oracle_lib, kind, N, Ts, T, B, w
         n_it += int(it_eq.sum())
         n += B
     assert n_it / n >= 0.95 and n_pol / n >= 0.95 and n_close / n >= 0.98, (n_it / n, n_pol / n, n_close / n)
+
+
+@pytest.fixture
+def split_from_21(gpu):
+    """Route 21 <= N <= 40 to the row-split kernel for one test (the step, per-step and fused closed loop), then back."""
+    prev = TB.SPLIT_MIN_N
+    TB.set_split_min_n(21)
+    try:
+        yield
+    finally:
+        TB.set_split_min_n(prev)
+
+
+@pytest.mark.parametrize("kind,N,T,B,warm", [("mixed", 40, 12, 48, 1), ("mixed", 40, 12, 48, 0), ("spline", 24, 10, 40, 1),
+                                             ("spline", 32, 8, 24, 0)])
+def test_split_fused_closed_loop_bit_identical(split_from_21, kind, N, T, B, warm):
+    """The row-split kernel's fused closed loop (queue, sc1 hand-off, in-workgroup linearization by block_linearize)
+    equals its per-step launches (rollout_kernel + jac_kernel + the closed-loop split solve) bit for bit -- histories,
+    statuses, iterations -- over two launches (the second ordered by the first, with the lead set), also with a grid far
+    smaller than B (many instances per workgroup)."""
+    from trajectory_generation_amd import _lib
+    from trajectory_generation_amd.workload import make_workload
+    Ts = 0.05
+    w = make_workload(B, N, Ts, kind=kind, seed=13)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=warm)
+    per = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
+    for grid in (0, 7):
+        dev = per["X"].device
+        x = torch.as_tensor(w["x0"], device=dev).clone()
+        u = torch.as_tensor(w["u0"], device=dev).clone()
+        vr = torch.as_tensor(np.tile(w["vref"], (B, 1)), device=dev)
+        hx = torch.empty((B, T + 1, 6), dtype=torch.float64, device=dev)
+        hu = torch.empty((B, T, 2), dtype=torch.float64, device=dev)
+        hx[:, 0] = x
+        st = torch.empty((T, B), dtype=torch.int32, device=dev)
+        it = torch.empty((T, B), dtype=torch.int32, device=dev)
+        T0 = T // 3
+        try:
+            _lib.check(_lib.lib().traj_debug_fused_grid(grid), "traj_debug_fused_grid")
+            TB.closed_loop_run(x, u, paths, vr, cfg, None, 0, T0, hx, hu, st[:T0], it[:T0])
+            TB.closed_loop_run(x, u, paths, vr, cfg, None, T0, T - T0, hx, hu, st[T0:], it[T0:])
+        finally:
+            _lib.lib().traj_debug_fused_grid(0)
+        assert _same(hx, per["X"]) and _same(hu, per["U"]), grid
+        assert torch.equal(st, per["status"]) and torch.equal(it, per["iters"]), grid
+
+
+def test_split_config3_per_step_vs_oracle(split_from_21, oracle_lib):
+    """Config 3 (mixed references, N = 40, dt = 0.05) on the row-split kernel: SURVEY.md 8(d) gate (1) as for the
+    capacity-80 kernel (test_closed_loop_per_step_parity_ts005): every step of the fused closed loop (cold rho),
+    re-solved from the GPU's state by the step entry point (the loop's u, bit for bit) and by the oracle: statuses
+    identical, u to 1e-6 where both polished, to 1e-3 where both stopped unpolished at the same iteration, iteration
+    counts equal on >= 95 %."""
+    from trajectory_generation_amd.workload import make_workload
+    N, Ts, T, B = 40, 0.05, 20, 32
+    w = make_workload(B, N, Ts, kind="mixed", seed=9)
+    paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
+    cfg = TB.config_struct(N=N, Ts=Ts, warm_start=0)
+    res = {k: v.cpu().numpy() for k, v in TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg).items()}
+    vr = np.tile(w["vref"], (B, 1))
+    n = n_it = n_pol = 0
+    for t in range(T):
+        xt = res["X"][:, t]
+        ut = res["U"][:, t - 1] if t > 0 else w["u0"]
+        prt = TB.ref_window_batch(paths, xt[:, 0], vr, N, Ts).cpu().numpy()
+        g = {k: v.cpu().numpy() for k, v in TB.mpc_step_batch(xt, ut, prt, vr, cfg).items()}
+        assert np.array_equal(g["u_cmd"], res["U"][:, t]) and np.array_equal(g["status"], res["status"][t])
+        ro = oracle_lib.mpc_step_batch(xt, ut, prt, vr, oracle_lib.cfg(N=N, Ts=Ts))
+        assert np.array_equal(g["status"], ro["status"]), (t, g["status"], ro["status"])
+        ok = g["status"] <= 1
+        pg, pr_ = g["polished"] > 0, ro["polished"] > 0
+        du = np.abs(g["u_cmd"] - ro["u_cmd"]).max(axis=1)
+        assert du[pg & pr_ & ok].max(initial=0.0) <= 1e-6, (t, du)
+        assert du[~pg & ~pr_ & ok & (g["iters"] == ro["iters"])].max(initial=0.0) <= 1e-3, (t, du)
+        n_it += int((g["iters"] == ro["iters"]).sum())
+        n_pol += int((pg == pr_).sum())
+        n += B
+    assert n_it / n >= 0.95 and n_pol / n >= 0.98, (n_it / n, n_pol / n)

@@ -116,6 +116,7 @@ _SIGS = {
     "traj_debug_fused_waves": (C.c_int, [C.c_int]),
     "traj_debug_step_linearize": (C.c_int, [C.c_int]),
     "traj_debug_split_max_n": (C.c_int, [C.c_int]),
+    "traj_debug_split_min_n": (C.c_int, [C.c_int]),
     "traj_debug_set_item_stamps": (C.c_int, [_V]),
     "traj_closed_loop_check": (C.c_int, [_V, C.c_size_t, C.c_int, C.c_int, _V]),
     "traj_dataset_write_csv": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_double, _V, _V, _V, _V,

@@ -91,6 +91,15 @@ struct KArgs {
     int wps;                 // fused: waves per SIMD of the kernel instance to launch (2, or 3 where built)
 };
 
+// Fused closed loop: coherent (sc1) stores and loads of an instance's state handed between workgroups on any XCD
+// (mpc_solve.h explains the protocol)
+__device__ __forceinline__ void st_coh(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coh(const double* p) {
+    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ double limit_scaling(double v) {
     return v < MIN_SCALING ? 1.0 : (v > MAX_SCALING ? MAX_SCALING : v);
 }

@@ -127,12 +127,7 @@ namespace tgmpc {
 // 200-step launch).  Instead (MI355X_MICROARCH.md, cross-workgroup publish): the state is stored with
 // coherent (sc1) stores, the storing lane waits for them (vmcnt(0)), then stores the step counter sc1;
 // the consumer polls the counter with sc1 loads and reads the state with sc1 loads.
-__device__ __forceinline__ void st_coh(double* p, double v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_coh(const double* p) {
-    return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+// (st_coh / ld_coh: mpc_common.h)
 
 // =====================================================================================
 // NN = capacity in QP variables (>= 2N); CLOSED = closed-loop step (window from the state, plant

@@ -24,17 +24,18 @@
 // polish only.  CLOSED: as mpc_long.h (window from the state, warm rho, plant update, history).
 #pragma once
 #include "mpc_common.h"
+#include "mpc_linearize.h"
 
 namespace tgmpc {
 
-// capacities built: H = 48 (n <= 96, 3 waves) and H = 64 (n <= 128, 4 waves)
+// capacities built: H = 40 (n <= 80, 3 waves: rows 80..95 idle), 48 (n <= 96, 3 waves), 64 (n <= 128, 4 waves)
 template <int H> struct SplitCfg {
     static constexpr int NR = 2 * H;                 // rows = columns capacity
     static constexpr int WAVES = (NR + 31) / 32;     // 32 rows per wave
     static constexpr int NT = 64 * WAVES;
     static constexpr int NRW = 32 * WAVES;           // row slots (>= NR)
 };
-__host__ __device__ inline int split_h(int n) { return n <= 96 ? 48 : 64; }
+__host__ __device__ inline int split_h(int n) { return n <= 80 ? 40 : (n <= 96 ? 48 : 64); }
 // per-instance scratch (doubles): the scaled P, NRW rows x 2H
 __host__ __device__ inline size_t split_ws_doubles(int N) {
     const int H = split_h(2 * N);
@@ -62,8 +63,16 @@ __device__ __forceinline__ double pair_max(double v) {   // NaN-propagating
     return (a > b || a != a) ? a : b;
 }
 
-template <int H, bool CLOSED = false>
-__global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void solve_split_kernel(const KArgs a, double* sws, size_t sstride) {
+// FUSED (the fused closed loop, traj_closed_loop_run; implies CLOSED): the grid is the resident workgroups, each takes
+// (step, instance) work items from the queue in order and waits, if it must, until the instance's previous step is
+// complete -- the protocol of mpc_solve.h's fused instances (sc1 state hand-off, the step counter stored after the
+// state, the lead set of heavy instances): the linearization runs in the workgroup (block_linearize, stage records in
+// LDS) and the P scratch is the workgroup's.  The same values as the per-step launches (rollout_kernel + jac_kernel +
+// this kernel), bit for bit.
+template <int H, bool CLOSED = false, bool FUSED = false>
+__global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void solve_split_kernel(
+    const KArgs a0, double* sws, size_t sstride) {
+    static_assert(!FUSED || CLOSED, "the fused run is the closed loop");
     using SC = SplitCfg<H>;
     constexpr int NR = SC::NR, NT = SC::NT, NRW = SC::NRW, WAVES = SC::WAVES;
     constexpr int PL = 2 * H;                 // P row stride (doubles)
@@ -71,20 +80,70 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     __shared__ __attribute__((aligned(16))) double s_bc[2][NRW];       // broadcast vectors (rotating)
     __shared__ double s_ex[4][NRW];                                    // +-2 exchanges (rotating)
     __shared__ __attribute__((aligned(16))) double s_pv[2][2][SPV];    // sweep: [pivot parity][half][slice]
-    __shared__ __attribute__((aligned(16))) double s_F[3][NRW];        // condensing: F_k rows
     __shared__ double s_red[WAVES * 8];
     __shared__ int s_flag[4];
     __shared__ double s_xc[CLOSED ? 6 : 1], s_uc[CLOSED ? 2 : 1], s_prc[CLOSED ? 3 * (NR / 2 + 1) : 1];
     __shared__ double s_xs[6 * (NR / 2 + 1)];                          // outputs: X by the linear model
-    __shared__ double s_lin[54 * (NR / 2)];                            // A_k | B_k | g_k of every stage (condensing)
-    const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    __shared__ __attribute__((aligned(16))) double s_Fb[8][3][NRW];    // condensing: F_k rows of a block of stages
+    __shared__ __attribute__((aligned(16))) double s_rec[FUSED ? LREC * (NR / 2) : 2];   // fused: the stage records
+    __shared__ int s_item;
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int r = 32 * wid + (lane & 31), h = lane >> 5;    // row, half
+    // the P scratch: per instance (one workgroup per instance), or per workgroup (fused: a workgroup solves one item
+    // at a time)
+    double* const Pg = sws + (size_t)blockIdx.x * sstride;   // scaled P, row r at Pg + r PL
+    for (bool more = true; more;) {
+    more = FUSED;
+    // fused: the arguments through a pointer the compiler cannot see through, so that nothing derived from them is
+    // hoisted out of the item loop (it would stay live across every solve and spill) -- mpc_solve.h's device
+    typedef __attribute__((address_space(4))) const KArgs* KArgsPtr;
+    KArgsPtr ap = FUSED ? (KArgsPtr)__builtin_amdgcn_kernarg_segment_ptr() : (KArgsPtr) nullptr;
+    if constexpr (FUSED) asm volatile("" : "+s"(ap));
+    const KArgs& a = FUSED ? *(const KArgs*)ap : a0;
+    int b = blockIdx.x, step = 0;
+    if constexpr (FUSED) {
+        // item q <-> (step, rank) in the queue order of mpc_solve.h: the heavy ranks' first lead steps, then level s =
+        // the heavy ranks' step s + lead and the light ranks' step s; an item only ever waits for one drawn before it
+        const int Bq = a.B, S = a.nsteps;
+        const int L = (a.lead_h > 0) ? min(a.lead_steps, S) : 0, Hh = (L > 0) ? a.lead_h : 0;
+        const int P0 = L * Hh, full = (S - L) * Bq;
+        __syncthreads();
+        if (t == 0) s_item = atomicAdd(&a.queue[0], 1);
+        __syncthreads();
+        const int q = s_item;
+        if (q >= Bq * S) break;
+        int rank;
+        if (q < P0) {
+            step = q / Hh;
+            rank = q - step * Hh;
+        } else if (q - P0 < full) {
+            const int lv = (q - P0) / Bq;
+            rank = (q - P0) - lv * Bq;
+            step = (rank < Hh) ? lv + L : lv;
+        } else {
+            const int q2 = q - P0 - full, lv = (S - L) + q2 / (Bq - Hh);
+            rank = Hh + (q2 - (lv - (S - L)) * (Bq - Hh));
+            step = lv;
+        }
+        b = a.perm ? a.perm[rank] : rank;
+        if (t == 0 && step > 0) {
+            int spins = 0;
+            while (__hip_atomic_load(&a.queue[2 + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < step) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > a.spin_limit) {   // bounded: a lost hand-off is reported (TRAJ_E_HANDOFF), never a hang
+                    __hip_atomic_store(&a.queue[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int tstep = a.t + step;
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
     const int N = c.N, n = 2 * N;
     const bool own = r < n;
     const int kk = r >> 1, ch = r & 1;
-    double* const Pg = sws + (size_t)b * sstride;            // scaled P, row r at Pg + r PL
     const double* vr = a.vref + (size_t)(N + 1) * b;
 
     // ---- block helpers ----
@@ -139,8 +198,13 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
 
     // ---- inputs (:144-163 normalisation by the caller; CLOSED: state, u_prev and the window) ----
     if constexpr (CLOSED) {
-        if (t < 6) s_xc[t] = a.x_state[6 * (size_t)b + t];
-        if (t < 2) s_uc[t] = a.u_state[2 * (size_t)b + t];
+        if (FUSED) {   // the state the instance's previous step published (sc1 loads, mpc_solve.h st_coh / ld_coh)
+            if (t < 6) s_xc[t] = ld_coh(a.x_state + 6 * (size_t)b + t);
+            if (t < 2) s_uc[t] = ld_coh(a.u_state + 2 * (size_t)b + t);
+        } else {
+            if (t < 6) s_xc[t] = a.x_state[6 * (size_t)b + t];
+            if (t < 2) s_uc[t] = a.u_state[2 * (size_t)b + t];
+        }
         __syncthreads();
         if (t == 0) {   // main.py:51-68: xs_{k+1} = xs_k + vref_k Ts (serial, as ref_window_kernel)
             double xs = s_xc[0];
@@ -161,11 +225,15 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     const double* x0 = CLOSED ? s_xc : a.x0 + 6 * (size_t)b;
     const double* up = CLOSED ? s_uc : a.u_prev + 2 * (size_t)b;
     const double* pref = CLOSED ? s_prc : a.path_ref + (size_t)3 * (N + 1) * b;
-    const double* gA = a.Ad + (size_t)36 * N * b;
-    const double* gB = a.Bd + (size_t)12 * N * b;
-    const double* gg = a.gd + (size_t)6 * N * b;
     if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
     __syncthreads();
+    // A_k, B_k, g_k: the workspace's (stage k at gA + RA k, ...), or, fused, the stage records the workgroup's own
+    // linearization leaves in LDS (block_linearize: rollout_kernel + jac_kernel's values, bit for bit)
+    if constexpr (FUSED) block_linearize<NT>(t, p, N, c.Ts, s_xc, s_uc, s_rec, nullptr);
+    constexpr int RA = FUSED ? LREC : 36, RB = FUSED ? LREC : 12, RG = FUSED ? LREC : 6;
+    const double* gA = FUSED ? s_rec : a.Ad + (size_t)36 * N * b;
+    const double* gB = FUSED ? s_rec + 36 : a.Bd + (size_t)12 * N * b;
+    const double* gg = FUSED ? s_rec + 48 : a.gd + (size_t)6 * N * b;
     {
         int bad = 0;
         if (t < 6) bad |= !isfinite(x0[t]);
@@ -183,63 +251,85 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     for (int i = 0; i < 6; ++i) xh[i] = x0[i];
     double qi = 0.0;
     double Kh[H];   // row r, columns of half h: P during condensing and scaling, then K and K^-1
-#pragma unroll
-    for (int i = 0; i < H; ++i) Kh[i] = 0.0;
-    // A_k, B_k, g_k staged in LDS (coalesced copy) and read back as uniform broadcasts as the stage loop needs them:
-    // read from global memory the compiler issues all 54 loads of a stage at once, beside the 2H registers of Kh
-    for (int i = t; i < 36 * N; i += NT) s_lin[i] = gA[i];
-    for (int i = t; i < 12 * N; i += NT) s_lin[36 * N + i] = gB[i];
-    for (int i = t; i < 6 * N; i += NT) s_lin[48 * N + i] = gg[i];
-    __syncthreads();
-    for (int k = 0; k < N; ++k) {
-        const double* Ak = s_lin + 36 * k;
-        const double* Bk = s_lin + 36 * N + 12 * k;
-        const double* gk = s_lin + 48 * N + 6 * k;
-        double xn[6], Gn[6];
-        for (int rr = 0; rr < 6; ++rr) {
-            double v = gk[rr], w = 0.0;
-            for (int cc = 0; cc < 6; ++cc) {
-                v = fma(Ak[6 * rr + cc], xh[cc], v);
-                w = fma(Ak[6 * rr + cc], G[cc], w);
+    // The stages in blocks of KB: first the block's sensitivities -- G_k, the free response, F_k (3 values of row r per
+    // stage, published to LDS) and q -- with no row of P live, then the block's products F_k' F_k added to the half-row,
+    // which lives in registers only in that second part (between blocks it is parked in the P scratch: the two parts'
+    // registers together do not fit two waves per SIMD).  The same FMAs in the same stage order as one pass.
+    constexpr int KB = 8;
+    double* const prow_s = Pg + (size_t)r * PL + h * H;   // this lane's half-row in the scratch
+    for (int k0 = 0; k0 < N; k0 += KB) {
+        const int kend = (k0 + KB < N) ? k0 + KB : N;
+        for (int k = k0; k < kend; ++k) {
+            const double* Ak = gA + RA * k;
+            double xn[6], Gn[6];
+            for (int rr = 0; rr < 6; ++rr) {
+                double v = gg[RG * k + rr], w = 0.0;
+                for (int cc = 0; cc < 6; ++cc) {
+                    v = fma(Ak[6 * rr + cc], xh[cc], v);
+                    w = fma(Ak[6 * rr + cc], G[cc], w);
+                }
+                xn[rr] = v;
+                Gn[rr] = (own && kk == k) ? gB[RB * k + 2 * rr + ch] : w;
             }
-            xn[rr] = v;
-            Gn[rr] = (own && kk == k) ? Bk[2 * rr + ch] : w;
+            for (int rr = 0; rr < 6; ++rr) { xh[rr] = xn[rr]; G[rr] = Gn[rr]; }
+            const int k1 = k + 1;
+            double sk, ck;
+            pm_sincos(pref[3 * k1 + 2], &sk, &ck);
+            const double e0 = sk * (xh[0] - pref[3 * k1]) - ck * (xh[1] - pref[3 * k1 + 1]);
+            const double e1 = xh[2] - pref[3 * k1 + 2];
+            const double e2 = xh[3] - vr[k1];
+            const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
+            qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
+            if (h == 0) {
+                s_Fb[k - k0][0][r] = F0;
+                s_Fb[k - k0][1][r] = F1;
+                s_Fb[k - k0][2][r] = F2;
+            }
         }
-        for (int rr = 0; rr < 6; ++rr) { xh[rr] = xn[rr]; G[rr] = Gn[rr]; }
-        const int k1 = k + 1;
-        double sk, ck;
-        pm_sincos(pref[3 * k1 + 2], &sk, &ck);
-        const double e0 = sk * (xh[0] - pref[3 * k1]) - ck * (xh[1] - pref[3 * k1 + 1]);
-        const double e1 = xh[2] - pref[3 * k1 + 2];
-        const double e2 = xh[3] - vr[k1];
-        const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
-        qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
-        if (h == 0) { s_F[0][r] = F0; s_F[1][r] = F1; s_F[2][r] = F2; }
         __syncthreads();
-        // F_k's columns >= 2 (k + 1) are zero (inputs of later stages; rows >= n hold F = 0): chunks of 8 columns from
-        // the first one that can be nonzero in half 0 (uniform skip); a half-1 lane's extra columns add exact zeros
-        const int jm = 2 * k + 2;
-        // (each chunk's 12 16-byte reads, then its 24 FMAs: the scheduler would otherwise issue every read first)
-        const double2* f2r[3] = {reinterpret_cast<const double2*>(&s_F[0][h * H]),
-                                 reinterpret_cast<const double2*>(&s_F[1][h * H]),
-                                 reinterpret_cast<const double2*>(&s_F[2][h * H])};
+        // the half-row back from the scratch (none before the first block); an opaque pointer, so that the compiler
+        // reloads it instead of keeping the stored values live across the sensitivity part
+        double* pp = prow_s;
+        asm volatile("" : "+v"(pp));
+        const double2* pp2 = reinterpret_cast<const double2*>(pp);
 #pragma unroll
-        for (int c0 = 0; c0 < H; c0 += 8) {
-            if (c0 >= jm) continue;
-            double2 f0[4], f1[4], f2[4];
+        for (int i = 0; i < H; i += 2) {
+            const double2 v2 = (k0 == 0) ? double2{0.0, 0.0} : pp2[i / 2];
+            Kh[i] = v2.x;
+            Kh[i + 1] = v2.y;
+        }
+        for (int k = k0; k < kend; ++k) {
+            const double F0 = s_Fb[k - k0][0][r], F1 = s_Fb[k - k0][1][r], F2 = s_Fb[k - k0][2][r];
+            // F_k's columns >= 2 (k + 1) are zero (inputs of later stages; rows >= n hold F = 0): chunks of 8 columns
+            // from the first one that can be nonzero in half 0 (uniform skip); a half-1 lane's extra columns add zeros
+            const int jm = 2 * k + 2;
+            // (each chunk's 12 16-byte reads, then its 24 FMAs: the scheduler would otherwise issue every read first)
+            const double2* f2r[3] = {reinterpret_cast<const double2*>(&s_Fb[k - k0][0][h * H]),
+                                     reinterpret_cast<const double2*>(&s_Fb[k - k0][1][h * H]),
+                                     reinterpret_cast<const double2*>(&s_Fb[k - k0][2][h * H])};
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                f0[i] = f2r[0][c0 / 2 + i];
-                f1[i] = f2r[1][c0 / 2 + i];
-                f2[i] = f2r[2][c0 / 2 + i];
+            for (int c0 = 0; c0 < H; c0 += 8) {
+                if (c0 >= jm) continue;
+                double2 f0[4], f1[4], f2[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    f0[i] = f2r[0][c0 / 2 + i];
+                    f1[i] = f2r[1][c0 / 2 + i];
+                    f2[i] = f2r[2][c0 / 2 + i];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    Kh[c0 + 2 * i] = fma(F0, f0[i].x, fma(F1, f1[i].x, fma(F2, f2[i].x, Kh[c0 + 2 * i])));
+                    Kh[c0 + 2 * i + 1] = fma(F0, f0[i].y, fma(F1, f1[i].y, fma(F2, f2[i].y, Kh[c0 + 2 * i + 1])));
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
             }
+        }
+        {   // park the half-row (after the last block too: the penalty band is added in the scratch, below)
+            double2* wp2 = reinterpret_cast<double2*>(pp);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                Kh[c0 + 2 * i] = fma(F0, f0[i].x, fma(F1, f1[i].x, fma(F2, f2[i].x, Kh[c0 + 2 * i])));
-                Kh[c0 + 2 * i + 1] = fma(F0, f0[i].y, fma(F1, f1[i].y, fma(F2, f2[i].y, Kh[c0 + 2 * i + 1])));
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
+            for (int i = 0; i < H; i += 2) wp2[i / 2] = double2{Kh[i], Kh[i + 1]};
         }
         __syncthreads();
     }
@@ -251,15 +341,31 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     const double Rd0 = ch ? Rds[2] : Rds[0], Rd1 = ch ? Rds[3] : Rds[1];
     const double dmul = (kk < N - 1) ? 2.0 : 1.0;
     if (own) {
-#pragma unroll
-        for (int i = 0; i < H; ++i) {
-            const int j = h * H + i, kj = j >> 1;
-            const double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
-            double add = (kj == kk) ? 2.0 * rs + 2.0 * rd * dmul : 0.0;
-            add = (j < n && (kj == kk - 1 || kj == kk + 1)) ? -2.0 * rd : add;
-            Kh[i] = (j < n && (kj >= kk - 1 && kj <= kk + 1)) ? Kh[i] + add : Kh[i];
+        // row r's band entries (columns 2 kk - 2 .. 2 kk + 3) in the scratch, by the half-0 lane (dynamic columns: no
+        // per-register selects), then both halves reload the row
+        if (h == 0) {
+            double* const pr_ = Pg + (size_t)r * PL;
+            const int j0 = 2 * kk - 2 > 0 ? 2 * kk - 2 : 0, j1 = 2 * kk + 4 < n ? 2 * kk + 4 : n;
+            for (int j = j0; j < j1; ++j) {
+                const int kj = j >> 1;
+                const double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
+                const double add = (kj == kk) ? 2.0 * rs + 2.0 * rd * dmul : -2.0 * rd;
+                pr_[j] = pr_[j] + add;
+            }
         }
         if (kk == 0) qi -= 2.0 * (Rd0 * up[0] + Rd1 * up[1]);
+    }
+    __syncthreads();
+    {
+        double* pp = prow_s;
+        asm volatile("" : "+v"(pp));
+        const double2* pp2 = reinterpret_cast<const double2*>(pp);
+#pragma unroll
+        for (int i = 0; i < H; i += 2) {
+            const double2 v2 = pp2[i / 2];
+            Kh[i] = v2.x;
+            Kh[i + 1] = v2.y;
+        }
     }
     // row maximum |P_rj| (both halves)
     auto row_absmax = [&]() -> double {
@@ -336,11 +442,11 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         qi *= cs;
         // the scaled P to the scratch (row r's half h at Pg + r PL + h H); the padding rows r >= n hold the identity
         // row there (zero otherwise), so that K's padding pivots are trivial
-        if (r < NR) {
+        {   // (the scratch holds NRW rows: padding rows past NR park there too, never read by a real row)
             double2* w2 = reinterpret_cast<double2*>(Pg + (size_t)r * PL + h * H);
 #pragma unroll
             for (int i = 0; i < H; i += 2) w2[i / 2] = double2{Kh[i], Kh[i + 1]};
-            if (!own && h == r / H) Pg[(size_t)r * PL + r] = 1.0;
+            if (!own && r < NR && h == r / H) Pg[(size_t)r * PL + r] = 1.0;
         }
         const double csinv = 1.0 / cs;
         const double D_dn = exch(D, -2);
@@ -364,17 +470,18 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         // (P v)_r: the half-row from the scratch (16-byte loads, all in flight), 4 chains, the pair sum
         auto Pmul = [&](double v) -> double {
             const double* vb = bcast(v);
+            const double2* v2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb + h * H, 16));
             double s4[4] = {0.0, 0.0, 0.0, 0.0};
-            const double2* p2 = reinterpret_cast<const double2*>(Pg + (size_t)(r < NR ? r : NR - 1) * PL + h * H);
+            const double2* p2 = reinterpret_cast<const double2*>(Pg + (size_t)r * PL + h * H);
 #pragma unroll
-            for (int i0 = 0; i0 < H; i0 += 16) {
-                double2 pv[8];
+            for (int i0 = 0; i0 < H; i0 += 8) {
+                double2 pv[4], vv[4];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) pv[i] = p2[i0 / 2 + i];
+                for (int i = 0; i < 4; ++i) { pv[i] = p2[i0 / 2 + i]; vv[i] = v2[i0 / 2 + i]; }
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    s4[(2 * i) & 3] = fma(pv[i].x, vb[h * H + i0 + 2 * i], s4[(2 * i) & 3]);
-                    s4[(2 * i + 1) & 3] = fma(pv[i].y, vb[h * H + i0 + 2 * i + 1], s4[(2 * i + 1) & 3]);
+                for (int i = 0; i < 4; ++i) {
+                    s4[(2 * i) & 3] = fma(pv[i].x, vv[i].x, s4[(2 * i) & 3]);
+                    s4[(2 * i + 1) & 3] = fma(pv[i].y, vv[i].y, s4[(2 * i + 1) & 3]);
                 }
             }
             const double s = pair_sum((s4[0] + s4[1]) + (s4[2] + s4[3]));
@@ -434,9 +541,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         constexpr int PH_ADMM = 0, PH_POLISH = 1, PH_DONE = 2;
         int phase = PH_ADMM;
         double rho = c.rho;
-        if (CLOSED && c.warm_start && a.t > 0 && a.wsWarm) {   // closed-loop warm start: the previous step's rho
+        if (CLOSED && c.warm_start && tstep > 0 && a.wsWarm) {   // closed-loop warm start: the previous step's rho
             const double* wv = a.wsWarm + 4 * (size_t)b;
-            if (wv[1] != 0.0) rho = fmin(fmax(wv[0], RHO_MIN), RHO_MAX);
+            const double w0 = FUSED ? ld_coh(wv) : wv[0], w1 = FUSED ? ld_coh(wv + 1) : wv[1];
+            if (w1 != 0.0) rho = fmin(fmax(w0, RHO_MIN), RHO_MAX);
         }
         double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
@@ -459,7 +567,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 // The band goes into P in the scratch (row r's half-0 lane adds its diagonal and its (r, r +- 2) entries),
                 // both lanes load the row half as it stands -- no per-entry selects (their masks, invariant across the
                 // solve, are what the compiler would hoist and spill) -- and the three entries are restored.
-                double* const prow = Pg + (size_t)(r < NR ? r : NR - 1) * PL;
+                double* const prow = Pg + (size_t)r * PL;
                 double o_dg = 0.0, o_sp = 0.0, o_sm = 0.0;
                 const bool has_sp = own && r + 2 < n, has_sm = own && has_prev;
                 if (own && h == 0) {
@@ -717,16 +825,24 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         xsol = D * x;
         if (CLOSED && a.wsWarm && t == 0) {
             double* wv = a.wsWarm + 4 * (size_t)b;
-            wv[0] = rho;
-            wv[1] = (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE) ? 1.0 : 0.0;
-            wv[2] = (double)iter;
+            const double w[3] = {rho, (status == TRAJ_STATUS_OPTIMAL || status == TRAJ_STATUS_OPTIMAL_INACCURATE) ? 1.0 : 0.0,
+                                 (double)iter};
+            for (int i = 0; i < 3; ++i) {
+                if (FUSED) st_coh(wv + i, w[i]);
+                else wv[i] = w[i];
+            }
         }
     } else {
         status = early;
         iter = 0;
         if (CLOSED && a.wsWarm && t == 0) {
-            a.wsWarm[4 * (size_t)b + 1] = 0.0;
-            a.wsWarm[4 * (size_t)b + 2] = 0.0;
+            if (FUSED) {
+                st_coh(a.wsWarm + 4 * (size_t)b + 1, 0.0);
+                st_coh(a.wsWarm + 4 * (size_t)b + 2, 0.0);
+            } else {
+                a.wsWarm[4 * (size_t)b + 1] = 0.0;
+                a.wsWarm[4 * (size_t)b + 2] = 0.0;
+            }
         }
     }
 
@@ -746,19 +862,38 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             f_cont(p, xs, u, f);
             for (int i = 0; i < 6; ++i) {
                 const double xn = xs[i] + c.Ts * f[i];
-                a.x_state[6 * (size_t)b + i] = xn;
-                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + a.t + 1) * 6 + i] = xn;
+                if (FUSED) st_coh(a.x_state + 6 * (size_t)b + i, xn);
+                else a.x_state[6 * (size_t)b + i] = xn;
+                if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + tstep + 1) * 6 + i] = xn;
             }
-            a.u_state[2 * (size_t)b] = uc0;
-            a.u_state[2 * (size_t)b + 1] = uc1;
+            if (FUSED) {
+                st_coh(a.u_state + 2 * (size_t)b, uc0);
+                st_coh(a.u_state + 2 * (size_t)b + 1, uc1);
+            } else {
+                a.u_state[2 * (size_t)b] = uc0;
+                a.u_state[2 * (size_t)b + 1] = uc1;
+            }
             if (a.hist_u) {
-                a.hist_u[((size_t)b * a.hist_T + a.t) * 2] = uc0;
-                a.hist_u[((size_t)b * a.hist_T + a.t) * 2 + 1] = uc1;
+                a.hist_u[((size_t)b * a.hist_T + tstep) * 2] = uc0;
+                a.hist_u[((size_t)b * a.hist_T + tstep) * 2 + 1] = uc1;
             }
-            if (a.status) a.status[b] = status;
-            if (a.iters) a.iters[b] = iter;
+            if (a.status) a.status[(size_t)step * a.B + b] = status;
+            if (a.iters) a.iters[(size_t)step * a.B + b] = iter;
+            if (FUSED) {
+                // mean iterations per step of this launch (the next launch's order), accumulated
+                if (a.wsWarm) {
+                    double* m = a.wsWarm + 4 * (size_t)b + 3;
+                    const double acc = (step == 0 ? 0.0 : ld_coh(m)) + iter;
+                    st_coh(m, (step == a.nsteps - 1) ? acc / a.nsteps : acc);
+                }
+                // hand the instance to whichever workgroup takes its next step: the sc1 state stores complete
+                // (vmcnt(0)), then the step counter is stored sc1
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&a.queue[2 + b], step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
-        return;
+        __syncthreads();
+        continue;
     }
     // X_{k+1} = A_k X_k + B_k U_k + g_k, stage by stage (thread i < 6: state i)
     double* const Xs = s_xs;
@@ -811,6 +946,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             const int rr = i / (N + 1), k = i % (N + 1);
             a.X_opt[(size_t)b * 6 * (N + 1) + i] = good ? Xs[6 * k + rr] : nan;
         }
+    }   // work items
 }
 
 }  // namespace tgmpc

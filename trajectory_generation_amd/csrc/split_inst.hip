@@ -7,22 +7,64 @@
 
 namespace tgmpc {
 
-// Row-split solve for TRAJ_MAX_N < N <= TRAJ_MAX_N_SPLIT: H = 48 (n <= 96, 3 waves) or 64 (n <= 128, 4 waves) per
-// instance.  sws: the caller's scratch (traj_mpc_sb_workspace_bytes), aligned up to 16 bytes here for the 16-byte P
-// row loads (B split_ws_doubles(N) + 2 <= B gen_ws_doubles(N) doubles: the slack fits).
+// sws: the caller's scratch (traj_mpc_sb_workspace_bytes), aligned up to 16 bytes here for the 16-byte P row loads
+// (B split_ws_doubles(N) + 2 <= B gen_ws_doubles(N) doubles: the slack fits)
+static double* align16(double* p) {
+    return reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
+}
+
+// Row-split solve for one launch of B instances (the step, the QP, one closed-loop step): H = 40 (n <= 80), 48
+// (n <= 96) or 64 (n <= 128), one workgroup of 32 rows per wave per instance
+template <int H, bool CLOSED>
+static int launch_one(const KArgs& a, double* al, size_t per, hipStream_t st) {
+    hipLaunchKernelGGL((solve_split_kernel<H, CLOSED>), dim3(a.B), dim3(SplitCfg<H>::NT), 0, st, a, al, per);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 template <bool CLOSED>
 static int launch_split_t(const KArgs& a, double* sws, hipStream_t st) {
-    const int N = a.c.N, n = 2 * N;
-    double* al = reinterpret_cast<double*>((reinterpret_cast<uintptr_t>(sws) + 15) & ~uintptr_t(15));
-    const size_t per = split_ws_doubles(N);
-    if (split_h(n) == 48)
-        hipLaunchKernelGGL((solve_split_kernel<48, CLOSED>), dim3(a.B), dim3(SplitCfg<48>::NT), 0, st, a, al, per);
-    else
-        hipLaunchKernelGGL((solve_split_kernel<64, CLOSED>), dim3(a.B), dim3(SplitCfg<64>::NT), 0, st, a, al, per);
+    const int n = 2 * a.c.N;
+    double* al = align16(sws);
+    const size_t per = split_ws_doubles(a.c.N);
+    if (split_h(n) == 40) return launch_one<40, CLOSED>(a, al, per, st);
+    if (split_h(n) == 48) return launch_one<48, CLOSED>(a, al, per, st);
+    return launch_one<64, CLOSED>(a, al, per, st);
+}
+
+// The fused closed loop (a.nsteps steps; the queue, order and lead set up by the caller): one workgroup per resident
+// slot (occupancy x CUs; at least ceil(B / TRAJ_FUSED_MAX_PER_WG), at most B), each with its own P scratch.  Per device
+// the slot count is asked of the occupancy API once.
+template <int H>
+static int launch_fused_h(const KArgs& a, double* al, size_t per, hipStream_t st) {
+    static int slots_per_cu[64] = {0};
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -3;
+    if (!slots_per_cu[dev]) {
+        int nb = 0, ncu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, solve_split_kernel<H, true, true>, SplitCfg<H>::NT, 0) !=
+                hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return -3;
+        slots_per_cu[dev] = nb < 1 ? 1 : nb;
+        cus[dev] = ncu < 1 ? 1 : ncu;
+    }
+    int G = a.fused_grid > 0 ? a.fused_grid : slots_per_cu[dev] * cus[dev];
+    if (G > a.B) G = a.B;
+    const int minG = (a.B + TRAJ_FUSED_MAX_PER_WG - 1) / TRAJ_FUSED_MAX_PER_WG;
+    if (G < minG) G = minG;
+    hipLaunchKernelGGL((solve_split_kernel<H, true, true>), dim3(G), dim3(SplitCfg<H>::NT), 0, st, a, al, per);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 int launch_split_step(const KArgs& a, double* sws, hipStream_t st) { return launch_split_t<false>(a, sws, st); }
 int launch_split_closed(const KArgs& a, double* sws, hipStream_t st) { return launch_split_t<true>(a, sws, st); }
+int launch_split_fused(const KArgs& a, double* sws, hipStream_t st) {
+    const int n = 2 * a.c.N;
+    double* al = align16(sws);
+    const size_t per = split_ws_doubles(a.c.N);
+    if (split_h(n) == 40) return launch_fused_h<40>(a, al, per, st);
+    if (split_h(n) == 48) return launch_fused_h<48>(a, al, per, st);
+    return launch_fused_h<64>(a, al, per, st);
+}
 
 }  // namespace tgmpc

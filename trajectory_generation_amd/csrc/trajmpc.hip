@@ -270,6 +270,7 @@ static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
 // other register-resident solvers): TRAJ_MAX_N < N <= TRAJ_MAX_N_SPLIT without state bounds
 int launch_split_step(const KArgs& a, double* sws, hipStream_t st);
 int launch_split_closed(const KArgs& a, double* sws, hipStream_t st);
+int launch_split_fused(const KArgs& a, double* sws, hipStream_t st);
 template <bool CLOSED>
 static int launch_split(const KArgs& a, double* sws, hipStream_t st) {
     return CLOSED ? launch_split_closed(a, sws, st) : launch_split_step(a, sws, st);
@@ -310,6 +311,13 @@ static int g_run_ahead = TGMPC_RUN_AHEAD;   // traj_debug_run_ahead
 // horizons up to which TRAJ_MAX_N < N runs the row-split kernel (mpc_split.h) instead of the long-horizon one
 // (traj_debug_split_max_n: 0 sends every N > TRAJ_MAX_N to the long-horizon kernel; the two agree to the step bars)
 static int g_split_max_n = TRAJ_MAX_N_SPLIT;
+// horizons from which the step / per-step closed loop run the row-split kernel (default TRAJ_MAX_N + 1: only past the
+// register-resident capacity; traj_debug_split_min_n lowers it to 21 for the experiments that compare it with the
+// capacity-80 kernel on the same inputs)
+static int g_split_min_n = TRAJ_MAX_N + 1;
+static bool split_route(const traj_mpc_config* c) {
+    return !state_bounds_active(c) && c->N >= g_split_min_n && c->N <= g_split_max_n;
+}
 // traj_debug_step_linearize: the step's linearization inside the solve launch.  An atomic: a test that flips it may run
 // beside other callers of the library; each traj_mpc_step_batch reads it once.
 static std::atomic<int> g_step_inlin{1};
@@ -364,6 +372,12 @@ int traj_debug_queue_lead(int steps, int per_mille) {
 int traj_debug_run_ahead(int levels) {
     if (levels < 0) return TRAJ_E_ARG;
     g_run_ahead = levels;
+    return TRAJ_OK;
+}
+
+int traj_debug_split_min_n(int n_min) {
+    if (n_min < 21 || n_min > TRAJ_MAX_N + 1) return TRAJ_E_ARG;
+    g_split_min_n = n_min;
     return TRAJ_OK;
 }
 
@@ -527,7 +541,7 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
     if (!lin && (!Ad || !Bd || !g)) return TRAJ_E_ARG;
     // the general solver: state bounds, or a horizon past the hot kernels' capacity (include/trajmpc.h tiers)
-    const bool sb = state_bounds_active(c) || c->N > TRAJ_MAX_N;
+    const bool sb = state_bounds_active(c) || c->N > TRAJ_MAX_N || split_route(c);
     const size_t base = lin ? ws_base_bytes(B, c->N) : 0;
     const size_t need = base + (sb ? traj_mpc_sb_workspace_bytes(B, c->N) : 0);
     if (need > 0 && (!ws || ws_bytes < need)) return TRAJ_E_ARG;
@@ -552,7 +566,7 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (lin && (sb || !inlin)) launch_linearize(a, (hipStream_t)stream, false);
     if (sb) {
         double* const sws = (double*)((char*)ws + base);
-        if (!state_bounds_active(c) && c->N <= g_split_max_n) return launch_split<false>(a, sws, (hipStream_t)stream);
+        if (split_route(c)) return launch_split<false>(a, sws, (hipStream_t)stream);
         if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long<false>(a, sws, (hipStream_t)stream);
         return launch_general(a, sws, (hipStream_t)stream);
     }
@@ -613,15 +627,16 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
 // solve_long_kernel); no state bounds (main.py passes none).  The long tier needs the step's scratch beside the
 // workspace, as the step entry point does: traj_mpc_workspace_bytes + traj_mpc_sb_workspace_bytes.
 static int check_cfg_closed(const traj_mpc_config* c) {
-    if (c && c->N > TRAJ_MAX_N && c->N <= TRAJ_MAX_N_LONG) {
+    if (c && ((c->N > TRAJ_MAX_N && c->N <= TRAJ_MAX_N_LONG) || split_route(c))) {
         const int e = check_cfg(c, true);
         if (e) return e;
         return state_bounds_active(c) ? TRAJ_E_UNSUPPORTED : TRAJ_OK;
     }
     return check_cfg(c);
 }
-static size_t closed_ws_bytes(int B, int N) {
-    return traj_mpc_workspace_bytes(B, N) + (N > TRAJ_MAX_N ? traj_mpc_sb_workspace_bytes(B, N) : 0);
+static size_t closed_ws_bytes(const traj_mpc_config* c, int B) {
+    const int N = c->N;
+    return traj_mpc_workspace_bytes(B, N) + ((N > TRAJ_MAX_N || split_route(c)) ? traj_mpc_sb_workspace_bytes(B, N) : 0);
 }
 // one long-horizon closed-loop step on a's state (a.t = the step, a.status / a.iters = this step's [B] rows)
 static int closed_step_long(const KArgs& a, void* ws, hipStream_t st) {
@@ -631,7 +646,7 @@ static int closed_step_long(const KArgs& a, void* ws, hipStream_t st) {
     stamp(2, st);
     stamp(3, st);
     double* const sws = (double*)((char*)ws + ws_base_bytes(a.B, a.c.N));
-    const int e = (a.c.N <= g_split_max_n) ? launch_split<true>(a, sws, st) : launch_long<true>(a, sws, st);
+    const int e = split_route(&a.c) ? launch_split<true>(a, sws, st) : launch_long<true>(a, sws, st);
     stamp(4, st);
     if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
     return e;
@@ -646,7 +661,7 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     if (e) return e;
     if (B == 0) return TRAJ_OK;
     if (!x || !u_prev || !vref) return TRAJ_E_ARG;
-    if (!workspace || workspace_bytes < closed_ws_bytes(B, c->N)) return TRAJ_E_ARG;
+    if (!workspace || workspace_bytes < closed_ws_bytes(c, B)) return TRAJ_E_ARG;
     if ((hist_x || hist_u) && (t < 0 || t >= hist_T)) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -666,7 +681,7 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.dbg = g_dbg;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
-    if (c->N > TRAJ_MAX_N) return closed_step_long(a, workspace, st);
+    if (c->N > TRAJ_MAX_N || split_route(c)) return closed_step_long(a, workspace, st);
     const int nr = (B + 63) / 64, nj = (B * c->N + 63) / 64;
     stamp(0, st);
     hipLaunchKernelGGL(rollout_kernel<true>, dim3(nr), dim3(64), 0, st, a);
@@ -695,7 +710,7 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     if (e) return e;
     if (B == 0 || steps == 0) return TRAJ_OK;
     if (!x || !u_prev || !vref || t0 < 0) return TRAJ_E_ARG;
-    if (!workspace || workspace_bytes < closed_ws_bytes(B, c->N)) return TRAJ_E_ARG;
+    if (!workspace || workspace_bytes < closed_ws_bytes(c, B)) return TRAJ_E_ARG;
     if ((hist_x || hist_u) && t0 + steps > hist_T) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -730,8 +745,8 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.queue = (int*)(a.wsWarm + (size_t)B * 4) + B;
     if (hipMemsetAsync(a.queue, 0, ((size_t)B * 2 + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
     a.run_ahead = g_run_ahead;
-    if (c->N > TRAJ_MAX_N) {
-        // past the register-resident capacity: the steps as long-horizon step launch sequences, in order on the stream
+    if (c->N > TRAJ_MAX_N && !split_route(c)) {
+        // past the row-split capacity: the steps as long-horizon step launch sequences, in order on the stream
         // (the same results as that many traj_closed_loop_step calls; the queue above stays clear, so
         // traj_closed_loop_check reports TRAJ_OK)
         for (int s = 0; s < steps; ++s) {
@@ -773,7 +788,9 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
         if (a.lead_h >= B) a.lead_h = B - 1;
     }
     stamp(3, st);
-    e = launch_mpc(a, st, 3);
+    // the row-split kernel's fused instance (the same queue protocol), or the register-resident one
+    e = split_route(c) ? launch_split_fused(a, (double*)((char*)workspace + ws_base_bytes(B, c->N)), st)
+                       : launch_mpc(a, st, 3);
     stamp(4, st);
     if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
     return e;
