@@ -57,6 +57,16 @@ def _capacity(n: int) -> int:
     return next(c for c in (16, 32, 40, 80) if n <= c)
 
 
+def _solve_kernel_name(N: int, fused: bool) -> str:
+    """The closed loop's solve kernel for horizon N (include/trajmpc.h tiers): the one-wave register-resident
+    solve_kernel up to N = 20, the row-split solve_split_kernel<H> for 21 <= N <= 64 (mpc_split.h)."""
+    n = 2 * N
+    if N < _lib.SPLIT_MIN_N:
+        return f"solve_kernel<{_capacity(n)},true>"
+    H = 40 if n <= 80 else (48 if n <= 96 else 64)
+    return f"solve_split_kernel<{H},true{',true' if fused else ''}>"
+
+
 def cpu_baseline(w, N, Ts, ntraj, nsteps, polish_mode, warm_start):
     """The oracle (oracle/, C restatement of the reference path + OSQP's ADMM) on host cores."""
     import oracle as O  # test infrastructure: used here only for the CPU-baseline leg
@@ -830,7 +840,7 @@ def mpc_leg(args, ops, dist, rank, world, N, kind, traffic_json, issue_json, sta
                 pass
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS if achieved is not None else None, "traffic": traffic,
-            "kernel": f"solve_kernel<{_capacity(2 * N)},true>" + (
+            "kernel": _solve_kernel_name(N, fused) + (
                 f" (fused closed loop, {steps_per_launch} steps per launch)" if fused else ""),
             "kernel_ms": kern_ms, "steps_per_launch": steps_per_launch,
             "bytes_per_launch": bytes_launch, "kernels_ms": kernels_ms, "traffic_step": traffic_step,

@@ -96,8 +96,10 @@ typedef struct {
 
 /* Horizon tiers (mpc_step takes any N, mpc_6stati.py:125):
  *   N <= TRAJ_MAX_N (40)                 the register-resident hot kernels (mpc_solve.h): every entry point;
- *   TRAJ_MAX_N < N <= TRAJ_MAX_N_SPLIT   without state bounds: the row-split kernel (mpc_split.h: K^-1 in registers, each
- *                                        row split across a lane pair joined by v_permlane32_swap, 2 waves per SIMD);
+ *   N <= 20                              the one-wave register-resident kernels (mpc_solve.h);
+ *   TRAJ_SPLIT_MIN_N <= N <= TRAJ_MAX_N_SPLIT  without state bounds: the row-split kernel (mpc_split.h: K^-1 in registers,
+ *                                        each row split across a lane pair joined by v_permlane32_swap, 2 waves per
+ *                                        SIMD; the QP entry point keeps the two-wave capacity-80 kernel up to TRAJ_MAX_N);
  *   TRAJ_MAX_N_SPLIT < N <= TRAJ_MAX_N_LONG  without state bounds: the long-horizon kernel (mpc_long.h: the hot kernels'
  *                                        algorithm with one thread per QP variable, K^-1 in LDS up to N = 64 and in
  *                                        the caller's scratch beyond);
@@ -110,7 +112,9 @@ typedef struct {
  * with the same extra scratch after the workspace; past TRAJ_MAX_N_LONG, or with state bounds, they return
  * TRAJ_E_UNSUPPORTED (main.py passes no state bounds). */
 #define TRAJ_MAX_N 40
-#define TRAJ_MAX_N_SPLIT 64      /* TRAJ_MAX_N < N <= this: the row-split kernel (mpc_split.h), K^-1 in registers */
+#define TRAJ_MAX_N_SPLIT 64      /* TRAJ_SPLIT_MIN_N <= N <= this: the row-split kernel (mpc_split.h), K^-1 rows in
+                                  * registers split across lane pairs */
+#define TRAJ_SPLIT_MIN_N 21
 #define TRAJ_MAX_N_LONG 128
 #define TRAJ_MAX_N_GENERAL 256
 
@@ -141,7 +145,8 @@ int traj_lateral_error_batch(int B, const double* X, const double* Y, const doub
  * (x_k, f_k) per stage (B * N * 12 doubles), then the closed-loop record of the previous step
  * (B * 4 doubles: rho, valid flag, ADMM iterations, mean iterations of the last fused run), the
  * closed-loop solve order (B ints, longest first) and the fused run's step queue (B + 2 ints).  Pass the same buffer to every traj_closed_loop_step of one run;
- * step t = 0 starts cold.  The closed loop at TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG needs traj_mpc_workspace_bytes(B, N) +
+ * step t = 0 starts cold.  For TRAJ_SPLIT_MIN_N <= N <= TRAJ_MAX_N_SPLIT the size includes the row-split kernel's scratch.
+ * The closed loop at TRAJ_MAX_N_SPLIT < N <= TRAJ_MAX_N_LONG needs traj_mpc_workspace_bytes(B, N) +
  * traj_mpc_sb_workspace_bytes(B, N) bytes (the long-horizon kernel's scratch after the workspace). */
 size_t traj_mpc_workspace_bytes(int B, int N);
 /* Scratch of the general solver, which runs with state bounds (x_lo / x_hi given with a finite side,
@@ -280,9 +285,9 @@ int traj_debug_step_linearize(int in_kernel);
  * long-horizon kernel (0: every N > TRAJ_MAX_N on the long-horizon kernel).  Both restate the same solver; for the
  * tests that compare them.  Diagnostics only. */
 int traj_debug_split_max_n(int n_max);
-/* Horizons n_min <= N <= TRAJ_MAX_N also run the row-split kernel on the step and per-step closed-loop paths (21 ..
- * TRAJ_MAX_N + 1; default TRAJ_MAX_N + 1 = none; the scratch of traj_mpc_sb_workspace_bytes is then needed as past
- * TRAJ_MAX_N).  For the experiments that compare it with the capacity-80 kernel.  Diagnostics only. */
+/* Horizons n_min <= N <= TRAJ_MAX_N run the row-split kernel on the step and closed-loop paths (21 .. TRAJ_MAX_N + 1;
+ * default TRAJ_SPLIT_MIN_N = 21; TRAJ_MAX_N + 1 = none, the capacity-80 kernel then runs 20 < N <= TRAJ_MAX_N).  For the
+ * experiments and tests that compare the two.  Diagnostics only. */
 int traj_debug_split_min_n(int n_min);
 
 #ifdef __cplusplus

@@ -117,8 +117,17 @@ def test_default_config_matches_oracle(L, oracle_lib):
 
 
 def test_workspace_bytes(L):
-    for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40)):
-        assert L.traj_mpc_workspace_bytes(B, N) == (B * N * 66 + 4 * B) * 8 + ((4 * (3 * B + 2) + 7) // 8) * 8
+    """The base part (A/B/g, stage records, warm records, order, queue) and, for the row-split kernel's horizons
+    (TRAJ_SPLIT_MIN_N <= N <= TRAJ_MAX_N_SPLIT, mpc_split.h), its P scratch: NRW x 2H doubles per instance + 16 bytes
+    of alignment slack (H = 40 / 48 / 64 by n = 2N; NRW = 32 rows per wave)."""
+    def split(B, N):
+        if not (_lib.SPLIT_MIN_N <= N <= _lib.MAX_N_SPLIT):
+            return 0
+        H = 40 if 2 * N <= 80 else (48 if 2 * N <= 96 else 64)
+        return (B * 32 * ((2 * H + 31) // 32) * 2 * H + 2) * 8
+    for B, N in ((0, 20), (1, 1), (4096, 20), (7, 40), (7, 21), (3, 48), (2, 64), (2, 65)):
+        assert L.traj_mpc_workspace_bytes(B, N) == ((B * N * 66 + 4 * B) * 8 + ((4 * (3 * B + 2) + 7) // 8) * 8
+                                                    + split(B, N)), (B, N)
     assert L.traj_mpc_workspace_bytes(-1, 20) == 0
 
 
@@ -162,13 +171,17 @@ def test_argument_errors_are_reported_before_any_launch(L):
         cN = _lib.default_config(20, 0.05)
         cN.N = N
         assert L.traj_mpc_step_batch(C.byref(p), C.byref(cN), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_E_ARG
-    # past the hot kernels' capacity: the step / QP entry points take it (general solver, caller-owned scratch:
-    # a workspace without it is refused before launching); the closed loop reports it as unsupported
+    # past the hot kernels' capacity: the step / QP entry points take it (the row-split kernel up to TRAJ_MAX_N_SPLIT,
+    # its scratch inside traj_mpc_workspace_bytes; past it the long-horizon / general solvers, their scratch after it:
+    # a workspace without it is refused before launching)
     cL = _lib.default_config(60, 0.05)
     assert L.traj_mpc_step_batch(C.byref(p), C.byref(cL), 0, *([nul] * 11), nul, 0, nul) == _lib.TRAJ_OK
     fk = C.c_void_p(16)
     assert L.traj_mpc_step_batch(C.byref(p), C.byref(cL), 4, *([fk] * 11), fk,
-                                 L.traj_mpc_workspace_bytes(4, 60), nul) == _lib.TRAJ_E_ARG
+                                 L.traj_mpc_workspace_bytes(4, 60) - 8, nul) == _lib.TRAJ_E_ARG
+    cLL = _lib.default_config(_lib.MAX_N_SPLIT + 1, 0.05)
+    assert L.traj_mpc_step_batch(C.byref(p), C.byref(cLL), 4, *([fk] * 11), fk,
+                                 L.traj_mpc_workspace_bytes(4, _lib.MAX_N_SPLIT + 1), nul) == _lib.TRAJ_E_ARG
     assert L.traj_mpc_qp_batch(C.byref(p), C.byref(cL), 4, *([fk] * 14), nul, 0, nul) == _lib.TRAJ_E_ARG
     assert L.traj_closed_loop_check(nul, 0, 4, 60, nul) == _lib.TRAJ_E_ARG
     # workspace too small (checked before launching)
@@ -192,14 +205,14 @@ def test_argument_errors_are_reported_before_any_launch(L):
     ps.kmax, ps.kind, ps.pc = 0, 16, 16                      # never dereferenced at B = 0
     assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 0, nul, nul, nul, 0, 0, nul, nul, nul,
                                    nul, nul, 0, nul) == _lib.TRAJ_E_UNSUPPORTED
-    # horizons past the hot kernels' capacity: the closed loop takes them up to TRAJ_MAX_N_LONG (the long-horizon
-    # kernel, whose scratch follows the workspace -- a workspace without it is an argument error before any launch);
-    # past that, or with state bounds, it reports them as unsupported, not as an argument error
-    cL = _lib.default_config(60, 0.05)
+    # horizons past the hot kernels' capacity: the closed loop takes them up to TRAJ_MAX_N_LONG (past TRAJ_MAX_N_SPLIT
+    # the long-horizon kernel, whose scratch follows the workspace -- a workspace without it is an argument error
+    # before any launch); past that, or with state bounds, it reports them as unsupported, not as an argument error
+    cL = _lib.default_config(_lib.MAX_N_SPLIT + 4, 0.05)
     cG = _lib.default_config(_lib.MAX_N_LONG + 1, 0.05)
     cLx = _lib.default_config(60, 0.05)
     cLx.has_x_lo, cLx.x_lo[3] = 1, -1.0
-    wsL = L.traj_mpc_workspace_bytes(4, 60)
+    wsL = L.traj_mpc_workspace_bytes(4, _lib.MAX_N_SPLIT + 4)
     for fn in (L.traj_closed_loop_step, L.traj_closed_loop_run):
         extra = (0, 1) if fn is L.traj_closed_loop_run else (0,)
         assert fn(C.byref(p), C.byref(cL), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,

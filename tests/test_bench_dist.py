@@ -137,7 +137,7 @@ def test_bench_world1_config3_host_io_and_profile_reasons(tmp_path, monkeypatch)
     assert out["roofline"]["issue"] is not None and out["roofline"]["issue"]["source"].endswith("sq.json")
     assert "not found" in out["roofline"]["traffic_rejected"]
     c3 = out["config3"]
-    assert c3["config"]["horizon"] == 40 and c3["value"] > 0 and c3["roofline"]["kernel"].startswith("solve_kernel<80")
+    assert c3["config"]["horizon"] == 40 and c3["value"] > 0 and c3["roofline"]["kernel"].startswith("solve_split_kernel<40,true,true>")
     assert c3["roofline"]["issue"] is None and "horizon = 20, this launch has 40" in c3["roofline"]["issue_rejected"]
     hio = out["host_io"]
     assert hio["value"] > 0 and hio["steps"] == 4 and hio["d2h_bytes"] == 4 * 5 * 6 * 8 + 4 * 4 * 2 * 8 + 2 * 4 * 4 * 4

@@ -45,6 +45,18 @@ def _oracle_gpu_tire_sine(oracle_lib):
         yield
 
 
+@pytest.fixture
+def cap80(gpu):
+    """Send 20 < N <= 40 to the two-wave capacity-80 kernel (mpc_solve.h) for one test (the library's default for those
+    horizons is the row-split kernel since round 6), then back: its instances keep their own bit-identity tests."""
+    prev = TB.SPLIT_MIN_N
+    TB.set_split_min_n(41)
+    try:
+        yield
+    finally:
+        TB.set_split_min_n(prev)
+
+
 def rel(a, b):
     return np.max(np.abs(np.asarray(a) - np.asarray(b)) / (1.0 + np.abs(np.asarray(b))))
 
@@ -431,12 +443,25 @@ def test_closed_loop_history_matches_single_steps(gpu):
         assert np.array_equal(res["X"].cpu().numpy()[:, t + 1], x)
 
 
-@pytest.mark.parametrize("N,warm,mode", [(20, 1, 0), (20, 0, 0), (8, 1, 0), (12, 1, 0), (30, 1, 0), (40, 1, 0),
-                                         (20, 1, 1)])
-def test_fused_closed_loop_bit_identical(gpu, N, warm, mode):
+@pytest.mark.parametrize("N,warm,mode,kernel", [(20, 1, 0, None), (20, 0, 0, None), (8, 1, 0, None), (12, 1, 0, None),
+                                                (30, 1, 0, 41), (40, 1, 0, 41), (30, 1, 0, 21), (40, 1, 1, 21),
+                                                (20, 1, 1, None)])
+def test_fused_closed_loop_bit_identical(gpu, N, warm, mode, kernel):
     """traj_closed_loop_run (one launch, in-workgroup linearization, on-chip state) equals the per-step
     launches bit for bit: histories, statuses, iteration counts; also when split into two runs.  Every
-    capacity: 16 (N 8), 32 (N 12), 40 (N 20), 80 (N 30 and N 40: 20 < N <= 40 runs the two-wave instance)."""
+    capacity: 16 (N 8), 32 (N 12), 40 (N 20), 80 (N 30 and N 40, kernel 41: the two-wave instance) and the row-split
+    kernel (kernel 21, the default for 20 < N <= 40)."""
+    from trajectory_generation_amd.workload import make_workload
+    prev = TB.SPLIT_MIN_N
+    if kernel is not None:
+        TB.set_split_min_n(kernel)
+    try:
+        _fused_closed_loop_bit_identical(gpu, N, warm, mode)
+    finally:
+        TB.set_split_min_n(prev)
+
+
+def _fused_closed_loop_bit_identical(gpu, N, warm, mode):
     from trajectory_generation_amd.workload import make_workload
     Ts, T, B = 0.05, 24, 96
     w = make_workload(B, N, Ts, kind="mixed" if N == 40 else "spline", seed=6)
@@ -499,7 +524,7 @@ def test_fused_three_waves_bit_identical(gpu, N, warm, mode):
             assert _same(per[k], r[k]), (wv, k)
 
 
-def test_fused_capacity80_instances_bit_identical(gpu):
+def test_fused_capacity80_instances_bit_identical(gpu, cap80):
     """Capacity 80 (N = 40, config 3): the one-wave-per-SIMD fused instance (the default) and the lean two-wave
     instance held to 2 waves per SIMD (traj_debug_fused_waves(2): 39 KB LDS, chunked reads) equal the per-step
     launches bit for bit, solver errors of the unstable N = 40 problems included."""
@@ -553,7 +578,7 @@ def test_fused_queue_lead_bit_identical(gpu, lead):
 
 
 @pytest.mark.parametrize("levels,grid", [(0, 0), (1, 28), (64, 0), (64, 28), (4, 12)])
-def test_fused_run_ahead_bit_identical(gpu, levels, grid):
+def test_fused_run_ahead_bit_identical(gpu, cap80, levels, grid):
     """Run-ahead (traj_debug_run_ahead: a workgroup keeps its instance for the next step, claimed once through the
     per-instance claim counter; drawers of run-ahead items draw again) moves only the schedule: two fused launches
     (the second ranked by the first) equal the per-step launches bit for bit, with every workgroup slot or a grid
@@ -932,12 +957,27 @@ def test_config3_hard_states_vs_fixture(gpu):
     assert du <= 1e-4, du
 
 
-def test_config3_iteration_cap_steps_vs_oracle(gpu, oracle_lib):
+@pytest.mark.parametrize("kernel", [41, 21])
+def test_config3_iteration_cap_steps_vs_oracle(gpu, oracle_lib, kernel):
     """Config 3's steps at the 10,000-iteration cap (the launch's tail): the bench's own N = 40
     mixed workload (4096 trajectories, dt = 0.05) run 25 steps by the fused closed loop with cold rho (the oracle's
     semantics); every step that ran to the cap (up to 12, spread over the run) is re-solved from the GPU's state by
     the oracle: the same status and the same 10,000 iterations, the u_prev fallback where the status is not optimal,
-    and u to 1e-3 where it is (an unpolished ADMM point after 10,000 iterations)."""
+    and u to 1e-3 where it is (an unpolished ADMM point after 10,000 iterations).  kernel 41: the capacity-80 kernel
+    (traj_debug_split_min_n(41)); kernel 21: the row-split kernel, the default since round 6.  On the row-split kernel
+    the status at the cap -- optimal_inaccurate or user_limit, OSQP's test of a NON-converged iterate's residuals
+    against 10 eps -- may flip between the two on a borderline step (its mat-vec sums in another order: half-row
+    partials joined across the lane pair); both still run the 10,000 iterations, and such a step is then compared by
+    that (u_prev where the GPU fell back, the GPU's u otherwise); at most one flip per sample."""
+    prev = TB.SPLIT_MIN_N
+    TB.set_split_min_n(kernel)
+    try:
+        _config3_iteration_cap_steps(oracle_lib, kernel)
+    finally:
+        TB.set_split_min_n(prev)
+
+
+def _config3_iteration_cap_steps(oracle_lib, kernel):
     from trajectory_generation_amd.workload import make_workload
     N, Ts, T, B = 40, 0.05, 25, 4096
     w = make_workload(B, N, Ts, kind="mixed")
@@ -949,6 +989,7 @@ def test_config3_iteration_cap_steps_vs_oracle(gpu, oracle_lib):
     cap = cap[np.linspace(0, len(cap) - 1, min(12, len(cap))).round().astype(int)]
     vr = np.tile(w["vref"], (B, 1))
     ocfg = oracle_lib.cfg(N=N, Ts=Ts)
+    flips = 0
     for t in np.unique(cap[:, 0]):
         bs = cap[cap[:, 0] == t, 1]
         xt = res["X"][:, t]
@@ -956,11 +997,17 @@ def test_config3_iteration_cap_steps_vs_oracle(gpu, oracle_lib):
         prt = TB.ref_window_batch(paths, xt[:, 0], vr, N, Ts).cpu().numpy()[bs]
         ro = oracle_lib.mpc_step_batch(xt[bs], ut[bs], prt, vr[bs], ocfg)
         gs, gu = res["status"][t, bs], res["U"][bs, t]
-        assert np.array_equal(gs, ro["status"]), (t, bs, gs, ro["status"])
+        same = gs == ro["status"]
+        if kernel == 41:
+            assert same.all(), (t, bs, gs, ro["status"])
+        else:   # a flip only between the two max_iter outcomes
+            assert np.isin(gs[~same], (1, 2)).all() and np.isin(ro["status"][~same], (1, 2)).all(), (t, bs, gs, ro["status"])
+            flips += int((~same).sum())
         assert np.array_equal(ro["iters"], np.full(len(bs), MAX_ITER)), (t, bs, ro["iters"])
         ok = gs <= 1
         assert np.array_equal(gu[~ok], ut[bs][~ok]), (t, bs)
-        assert np.abs(gu[ok] - ro["u_cmd"][ok]).max(initial=0.0) <= 1e-3, (t, bs)
+        assert np.abs(gu[ok & same] - ro["u_cmd"][ok & same]).max(initial=0.0) <= 1e-3, (t, bs)
+    assert flips <= 1, flips
 
 
 def test_divergent_dataset_trajectory_step_gate(gpu, oracle_lib):

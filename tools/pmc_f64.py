@@ -34,7 +34,7 @@ def main():
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 kn = row.get("Kernel_Name", "")
-                if "solve_kernel" in kn and "true, true" in kn and row.get("Counter_Name") in NAMES:
+                if ("solve_kernel" in kn or "solve_split_kernel" in kn) and "true, true" in kn and row.get("Counter_Name") in NAMES:
                     per[row["Dispatch_Id"]][row["Counter_Name"]] += float(row["Counter_Value"])
     if not per:
         raise SystemExit("no fused solve_kernel dispatch")

@@ -19,7 +19,7 @@ def largest(d):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 kn = row.get("Kernel_Name", "")
-                if "solve_kernel" in kn and "true, true" in kn:
+                if ("solve_kernel" in kn or "solve_split_kernel" in kn) and "true, true" in kn:
                     per[row["Dispatch_Id"]][row["Counter_Name"]] += float(row["Counter_Value"])
     return max(per.values(), key=lambda c: max(c.values()))
 

@@ -32,7 +32,8 @@ def read_counter_fused(d, name):
     for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if row.get("Counter_Name") == name and "solve_kernel" in row.get("Kernel_Name", "") \
+                if row.get("Counter_Name") == name and ("solve_kernel" in row.get("Kernel_Name", "")
+                                                        or "solve_split_kernel" in row.get("Kernel_Name", "")) \
                         and "true, true" in row.get("Kernel_Name", ""):
                     vals[row.get("Dispatch_Id")] += float(row["Counter_Value"])
     if not vals:

@@ -53,13 +53,13 @@ def step_compare(N, B, Ts=0.05):
           flush=True)
 
 
-def config3(N=40, B=4096, Ts=0.05, W=5, K=20):
-    w = make_workload(B, N, Ts, kind="mixed", seed=0)
+def config3(N=40, B=4096, Ts=0.05, W=5, K=20, kind="mixed", tail=True):
+    w = make_workload(B, N, Ts, kind=kind, seed=0)
     paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
     cfg = TB.config_struct(N=N, Ts=Ts, warm_start=1)
     res = {}
-    for name, split, fused in (("cap80_fused", 41, True), ("split_fused", 21, True), ("cap80_fused", 41, True),
-                               ("split_fused", 21, True), ("split_per_step", 21, False)):
+    runs = (("cap80_fused", 41, True), ("split_fused", 21, True), ("cap80_fused", 41, True), ("split_fused", 21, True))
+    for name, split, fused in runs + ((("split_per_step", 21, False),) if tail else ()):
         TB.set_split_min_n(split)
         x = torch.as_tensor(w["x0"], device="cuda").clone()
         u = torch.as_tensor(w["u0"], device="cuda").clone()
@@ -85,7 +85,7 @@ def config3(N=40, B=4096, Ts=0.05, W=5, K=20):
         dt = time.perf_counter() - t0
         sth = st[W:].cpu().numpy().reshape(-1)
         res[name] = (hx.cpu().numpy(), hu.cpu().numpy(), it.cpu().numpy())
-        print(json.dumps({"what": "config 3 closed loop", "path": name, "value": B * K / dt, "ms": dt * 1e3,
+        print(json.dumps({"what": f"fused closed loop, {kind}, N = {N}", "path": name, "value": B * K / dt, "ms": dt * 1e3,
                           "iters_mean": float(it[W:].float().mean()),
                           "status_hist": np.bincount(sth, minlength=7).tolist()}), flush=True)
     TB.set_split_min_n(41)
@@ -93,7 +93,7 @@ def config3(N=40, B=4096, Ts=0.05, W=5, K=20):
     # cold start reaches the cap too) on each kernel -- its per-iteration latency
     hxa, hua, ita = res["cap80_fused"]
     cap = np.argwhere(ita == 10000)
-    if len(cap):
+    if len(cap) and tail:
         t, bb = cap[0]
         x0 = hxa[bb, t][None]
         u0 = (hua[bb, t - 1] if t > 0 else np.asarray(w["u0"])[bb])[None]
@@ -116,6 +116,9 @@ def main():
         if N > 0:
             for B in (1024, 4096):
                 step_compare(N, B)
+    if "--horizons" in sys.argv:
+        for N in (24, 32, 40):
+            config3(N=N, kind="spline", tail=False)
     config3()
 
 

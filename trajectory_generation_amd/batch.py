@@ -158,12 +158,13 @@ def _state_bounds(cfg: MpcConfig) -> bool:
     return any((cfg.has_x_lo and cfg.x_lo[i] > -1e30) or (cfg.has_x_hi and cfg.x_hi[i] < 1e30) for i in range(6))
 
 
-# horizons from which the row-split kernel runs (traj_debug_split_min_n; MAX_N + 1 unless an experiment lowers it)
-SPLIT_MIN_N = _lib.MAX_N + 1
+# horizons from which the row-split kernel runs (traj_debug_split_min_n; the library default TRAJ_SPLIT_MIN_N)
+SPLIT_MIN_N = _lib.SPLIT_MIN_N
 
 
 def set_split_min_n(n_min: int) -> None:
-    """Experiments: run the row-split kernel from horizon n_min on (step and per-step closed loop; 21 .. MAX_N + 1)."""
+    """Experiments: run the row-split kernel from horizon n_min on (step and closed loop; 21 .. MAX_N + 1, the latter
+    sending 20 < N <= MAX_N back to the capacity-80 kernel).  The workspace sizes do not depend on it."""
     global SPLIT_MIN_N
     _lib.check(_lib.lib().traj_debug_split_min_n(int(n_min)), "traj_debug_split_min_n")
     SPLIT_MIN_N = int(n_min)
@@ -172,7 +173,7 @@ def set_split_min_n(n_min: int) -> None:
 def _general(cfg: MpcConfig) -> bool:
     """The step needs caller-owned scratch (traj_mpc_sb_workspace_bytes): state bounds, or a horizon past the hot
     kernels' capacity (MAX_N < N <= MAX_N_GENERAL, include/trajmpc.h's tiers) or routed to the row-split kernel."""
-    return _state_bounds(cfg) or cfg.N > _lib.MAX_N or cfg.N >= SPLIT_MIN_N
+    return _state_bounds(cfg) or cfg.N > _lib.MAX_N
 
 
 def workspace(B: int, N: int, device, extra_bytes: int = 0, role: str = "closed_loop") -> torch.Tensor:
@@ -336,7 +337,7 @@ def ref_window_batch(paths: PathSet, x_start, vref, N, Ts) -> torch.Tensor:
 def _closed_extra(B: int, N: int) -> int:
     """The closed loop past the register-resident capacity (MAX_N < N <= MAX_N_LONG) runs the long-horizon kernel one
     step per launch sequence; its scratch follows the workspace (traj_mpc_sb_workspace_bytes), as for the step."""
-    return int(_lib.lib().traj_mpc_sb_workspace_bytes(int(B), int(N))) if (N > _lib.MAX_N or N >= SPLIT_MIN_N) else 0
+    return int(_lib.lib().traj_mpc_sb_workspace_bytes(int(B), int(N))) if N > _lib.MAX_N_SPLIT else 0
 
 
 def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None, t=0, hist_x=None, hist_u=None,

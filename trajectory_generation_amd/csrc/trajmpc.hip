@@ -14,6 +14,7 @@
 #include "mpc_common.h"
 #include "mpc_general.h"
 #include "mpc_long.h"
+#include "mpc_split.h"   // (split_ws_doubles; the kernels are instantiated in split_inst.hip)
 #include "mpc_linearize.h"
 #include "physics.h"
 
@@ -311,12 +312,19 @@ static int g_run_ahead = TGMPC_RUN_AHEAD;   // traj_debug_run_ahead
 // horizons up to which TRAJ_MAX_N < N runs the row-split kernel (mpc_split.h) instead of the long-horizon one
 // (traj_debug_split_max_n: 0 sends every N > TRAJ_MAX_N to the long-horizon kernel; the two agree to the step bars)
 static int g_split_max_n = TRAJ_MAX_N_SPLIT;
-// horizons from which the step / per-step closed loop run the row-split kernel (default TRAJ_MAX_N + 1: only past the
-// register-resident capacity; traj_debug_split_min_n lowers it to 21 for the experiments that compare it with the
-// capacity-80 kernel on the same inputs)
-static int g_split_min_n = TRAJ_MAX_N + 1;
+// horizons from which the step and the closed loop (fused and per step) run the row-split kernel: default
+// TRAJ_SPLIT_MIN_N = 21, so that 20 < N <= TRAJ_MAX_N_SPLIT all run it -- at config 3 (N = 40, mixed references) it is
+// 1.09-1.10 M steps/s against the capacity-80 kernel's 1.02 M (its iteration-cap chains at 0.76 instead of 1.16 us per
+// ADMM iteration), within +-3 % of it on spline references at N = 24 / 32 / 40 (profiles/r06_split_probe*.json);
+// traj_debug_split_min_n(TRAJ_MAX_N + 1) sends 20 < N <= TRAJ_MAX_N back to the capacity-80 kernel
+static int g_split_min_n = TRAJ_SPLIT_MIN_N;
 static bool split_route(const traj_mpc_config* c) {
     return !state_bounds_active(c) && c->N >= g_split_min_n && c->N <= g_split_max_n;
+}
+// the row-split kernel's P scratch inside the workspace (after the base part): every horizon it can run, whatever the
+// routing, so that traj_mpc_workspace_bytes does not depend on a debug switch
+static size_t split_bytes(int B, int N) {
+    return (N >= 21 && N <= TRAJ_MAX_N_SPLIT) ? ((size_t)B * split_ws_doubles(N) + 2) * sizeof(double) : 0;
 }
 // traj_debug_step_linearize: the step's linearization inside the solve launch.  An atomic: a test that flips it may run
 // beside other callers of the library; each traj_mpc_step_batch reads it once.
@@ -540,10 +548,18 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (B == 0) return TRAJ_OK;
     if (!x0 || !u_prev || !path_ref || !vref || !u_cmd || !status) return TRAJ_E_ARG;
     if (!lin && (!Ad || !Bd || !g)) return TRAJ_E_ARG;
-    // the general solver: state bounds, or a horizon past the hot kernels' capacity (include/trajmpc.h tiers)
-    const bool sb = state_bounds_active(c) || c->N > TRAJ_MAX_N || split_route(c);
+    // which solver (include/trajmpc.h tiers): the general one (state bounds, or N > TRAJ_MAX_N_LONG), the long-horizon
+    // one (TRAJ_MAX_N_SPLIT < N <= TRAJ_MAX_N_LONG), the row-split one (split_route; the QP entry point up to TRAJ_MAX_N
+    // keeps the capacity-80 kernel, which needs no scratch), or the register-resident ones.  Scratch: the step's
+    // workspace holds the row-split kernel's (traj_mpc_workspace_bytes); the others' follows it (+ sb bytes), as does
+    // the QP entry point's whole scratch
+    const bool use_split = split_route(c) && (lin || c->N > TRAJ_MAX_N);
+    const bool gen_long = state_bounds_active(c) || (c->N > TRAJ_MAX_N && !use_split);
+    const bool sb = gen_long || use_split;
     const size_t base = lin ? ws_base_bytes(B, c->N) : 0;
-    const size_t need = base + (sb ? traj_mpc_sb_workspace_bytes(B, c->N) : 0);
+    const size_t need = lin ? base + (gen_long ? traj_mpc_sb_workspace_bytes(B, c->N)
+                                               : (use_split ? split_bytes(B, c->N) : 0))
+                            : (sb ? traj_mpc_sb_workspace_bytes(B, c->N) : 0);
     if (need > 0 && (!ws || ws_bytes < need)) return TRAJ_E_ARG;
     KArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -566,7 +582,7 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     if (lin && (sb || !inlin)) launch_linearize(a, (hipStream_t)stream, false);
     if (sb) {
         double* const sws = (double*)((char*)ws + base);
-        if (split_route(c)) return launch_split<false>(a, sws, (hipStream_t)stream);
+        if (use_split) return launch_split<false>(a, sws, (hipStream_t)stream);
         if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long<false>(a, sws, (hipStream_t)stream);
         return launch_general(a, sws, (hipStream_t)stream);
     }
@@ -582,7 +598,7 @@ static size_t ws_base_bytes(int B, int N) {
 
 size_t traj_mpc_workspace_bytes(int B, int N) {
     if (B < 0 || N < 0) return 0;
-    return ws_base_bytes(B, N);
+    return ws_base_bytes(B, N) + split_bytes(B, N);
 }
 
 size_t traj_mpc_sb_workspace_bytes(int B, int N) {
@@ -635,8 +651,8 @@ static int check_cfg_closed(const traj_mpc_config* c) {
     return check_cfg(c);
 }
 static size_t closed_ws_bytes(const traj_mpc_config* c, int B) {
-    const int N = c->N;
-    return traj_mpc_workspace_bytes(B, N) + ((N > TRAJ_MAX_N || split_route(c)) ? traj_mpc_sb_workspace_bytes(B, N) : 0);
+    const int N = c->N;   // (the row-split kernel's scratch is in traj_mpc_workspace_bytes; the long-horizon one's follows)
+    return traj_mpc_workspace_bytes(B, N) + ((N > TRAJ_MAX_N && !split_route(c)) ? traj_mpc_sb_workspace_bytes(B, N) : 0);
 }
 // one long-horizon closed-loop step on a's state (a.t = the step, a.status / a.iters = this step's [B] rows)
 static int closed_step_long(const KArgs& a, void* ws, hipStream_t st) {
