@@ -737,11 +737,12 @@ def test_long_horizon_exact_mode_and_qp_batch_vs_oracle(gpu, oracle_lib, N, Ts, 
         assert np.array_equal(q["u_cmd"][okq], q["U_opt"][okq][:, :, 0])
 
 
-@pytest.mark.parametrize("N,Ts", [(8, 0.05), (20, 0.05), (20, 0.02), (30, 0.05), (40, 0.05)])
+@pytest.mark.parametrize("N,Ts", [(8, 0.05), (20, 0.05), (20, 0.02), (30, 0.05), (40, 0.05), (48, 0.05), (64, 0.05)])
 def test_step_in_kernel_linearization_bit_identical(gpu, N, Ts):
-    """traj_mpc_step_batch runs the linearization inside the solve launch (one launch per call, block_linearize's
-    stage records copied to the workspace for X_opt); it equals the rollout_kernel + jac_kernel + solve sequence bit
-    for bit in every output, at every kernel capacity (16, 40, 80: N 30 and 40)."""
+    """traj_mpc_step_batch runs the linearization inside the solve launch (one launch per call; the capacity-16/40
+    kernels copy block_linearize's stage records to the workspace for X_opt, the row-split kernel reads them from LDS);
+    it equals the rollout_kernel + jac_kernel + solve sequence bit for bit in every output, at every kernel (capacity
+    16 and 40; the row-split kernel at H = 40 (N 30, 40), 48 and 64)."""
     from trajectory_generation_amd import _lib
     x0, up, pr, vr = random_instances(23, 48, N, Ts)
     cfg = TB.config_struct(N=N, Ts=Ts)

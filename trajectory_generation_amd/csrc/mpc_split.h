@@ -69,23 +69,36 @@ __device__ __forceinline__ double pair_max(double v) {   // NaN-propagating
 // state, the lead set of heavy instances): the linearization runs in the workgroup (block_linearize, stage records in
 // LDS) and the P scratch is the workgroup's.  The same values as the per-step launches (rollout_kernel + jac_kernel +
 // this kernel), bit for bit.
-template <int H, bool CLOSED = false, bool FUSED = false>
+// INLIN (implied by FUSED; the step entry point's default, traj_debug_step_linearize): the same in-workgroup
+// linearization for a step launch -- one launch per call instead of rollout_kernel + jac_kernel + this kernel, the
+// drop-in call's latency; bit-identical to the three-launch sequence.
+#ifndef TGMPC_SPLIT_GHOST
+#define TGMPC_SPLIT_GHOST 1
+#endif
+constexpr bool SPLIT_GHOST = TGMPC_SPLIT_GHOST != 0;
+// DIAG (fused only, when a diagnostic buffer is set: traj_debug_set_stamps): per-phase s_memtime stamps of each
+// instance's last step in a.dbg[b][0..11] (tools/split_phase.py); the production instances compile none of it.
+template <int H, bool CLOSED = false, bool FUSED = false, bool INLIN = FUSED, bool DIAG = false>
 __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu(2))) void solve_split_kernel(
     const KArgs a0, double* sws, size_t sstride) {
     static_assert(!FUSED || CLOSED, "the fused run is the closed loop");
+    static_assert(!FUSED || INLIN, "the fused run linearizes in the workgroup");
     using SC = SplitCfg<H>;
     constexpr int NR = SC::NR, NT = SC::NT, NRW = SC::NRW, WAVES = SC::WAVES;
     constexpr int PL = 2 * H;                 // P row stride (doubles)
     constexpr int SPV = 2 * H + 2;            // one pivot-row slice buffer: [off + m], m < 2H, off in {0, 1}
     __shared__ __attribute__((aligned(16))) double s_bc[2][NRW];       // broadcast vectors (rotating)
     __shared__ double s_ex[4][NRW];                                    // +-2 exchanges (rotating)
+    // ADMM: every row's constants of the rate-row update, read by the row two below it (the ghost update, below)
+    __shared__ __attribute__((aligned(16))) double s_gh[SPLIT_GHOST ? NRW + 2 : 1][6];
     __shared__ __attribute__((aligned(16))) double s_pv[2][2][SPV];    // sweep: [pivot parity][half][slice]
     __shared__ double s_red[WAVES * 8];
     __shared__ int s_flag[4];
-    __shared__ double s_xc[CLOSED ? 6 : 1], s_uc[CLOSED ? 2 : 1], s_prc[CLOSED ? 3 * (NR / 2 + 1) : 1];
+    __shared__ double s_xc[CLOSED || INLIN ? 6 : 1], s_uc[CLOSED || INLIN ? 2 : 1];
+    __shared__ double s_prc[CLOSED ? 3 * (NR / 2 + 1) : 1];
     __shared__ double s_xs[6 * (NR / 2 + 1)];                          // outputs: X by the linear model
     __shared__ __attribute__((aligned(16))) double s_Fb[8][3][NRW];    // condensing: F_k rows of a block of stages
-    __shared__ __attribute__((aligned(16))) double s_rec[FUSED ? LREC * (NR / 2) : 2];   // fused: the stage records
+    __shared__ __attribute__((aligned(16))) double s_rec[INLIN ? LREC * (NR / 2) : 2];   // INLIN: the stage records
     __shared__ int s_item;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int r = 32 * wid + (lane & 31), h = lane >> 5;    // row, half
@@ -139,6 +152,14 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         __syncthreads();
     }
     const int tstep = a.t + step;
+    // diagnostics: slot i of this instance's record, written by thread 0 at the launch's last step (DIAG only)
+    long long* const dbg = (DIAG && t == 0 && (!FUSED || step == a.nsteps - 1)) ? a.dbg : nullptr;
+    auto stamp = [&](int i, long long v) {
+        if (DIAG && dbg) dbg[(size_t)b * 32 + i] = v;
+    };
+    [[maybe_unused]] long long cyc_sweep = 0, cyc_pol = 0, t_prev = 0;
+    [[maybe_unused]] int n_fact = 0, ph_prev = -1;
+    stamp(0, __builtin_amdgcn_s_memtime());
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
     const int N = c.N, n = 2 * N;
@@ -222,18 +243,24 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             s_prc[3 * k + 2] = pm_atan(dy);
         }
     }
-    const double* x0 = CLOSED ? s_xc : a.x0 + 6 * (size_t)b;
-    const double* up = CLOSED ? s_uc : a.u_prev + 2 * (size_t)b;
+    if constexpr (INLIN && !CLOSED) {   // the step's state and input, staged for block_linearize
+        if (t < 6) s_xc[t] = a.x0[6 * (size_t)b + t];
+        if (t < 2) s_uc[t] = a.u_prev[2 * (size_t)b + t];
+    }
+    const double* x0 = (CLOSED || INLIN) ? s_xc : a.x0 + 6 * (size_t)b;
+    const double* up = (CLOSED || INLIN) ? s_uc : a.u_prev + 2 * (size_t)b;
     const double* pref = CLOSED ? s_prc : a.path_ref + (size_t)3 * (N + 1) * b;
     if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
     __syncthreads();
     // A_k, B_k, g_k: the workspace's (stage k at gA + RA k, ...), or, fused, the stage records the workgroup's own
     // linearization leaves in LDS (block_linearize: rollout_kernel + jac_kernel's values, bit for bit)
-    if constexpr (FUSED) block_linearize<NT>(t, p, N, c.Ts, s_xc, s_uc, s_rec, nullptr);
-    constexpr int RA = FUSED ? LREC : 36, RB = FUSED ? LREC : 12, RG = FUSED ? LREC : 6;
-    const double* gA = FUSED ? s_rec : a.Ad + (size_t)36 * N * b;
-    const double* gB = FUSED ? s_rec + 36 : a.Bd + (size_t)12 * N * b;
-    const double* gg = FUSED ? s_rec + 48 : a.gd + (size_t)6 * N * b;
+    stamp(1, __builtin_amdgcn_s_memtime());
+    if constexpr (INLIN) block_linearize<NT>(t, p, N, c.Ts, s_xc, s_uc, s_rec, nullptr);
+    stamp(2, __builtin_amdgcn_s_memtime());
+    constexpr int RA = INLIN ? LREC : 36, RB = INLIN ? LREC : 12, RG = INLIN ? LREC : 6;
+    const double* gA = INLIN ? s_rec : a.Ad + (size_t)36 * N * b;
+    const double* gB = INLIN ? s_rec + 36 : a.Bd + (size_t)12 * N * b;
+    const double* gg = INLIN ? s_rec + 48 : a.gd + (size_t)6 * N * b;
     {
         int bad = 0;
         if (t < 6) bad |= !isfinite(x0[t]);
@@ -402,6 +429,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();
     const int early = s_flag[0] ? TRAJ_STATUS_SOLVER_ERROR : (s_flag[1] ? TRAJ_STATUS_INFEASIBLE : -1);
+    stamp(3, __builtin_amdgcn_s_memtime());
     int status = TRAJ_STATUS_SOLVER_ERROR, iter = 0, pol = 0;
     double xsol = 0.0;
 
@@ -547,13 +575,21 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             if (w1 != 0.0) rho = fmin(fmax(w0, RHO_MIN), RHO_MAX);
         }
         double x = 0.0, zb = 0.0, zr = 0.0, yb = 0.0, yr = 0.0;
+        double zr_g = 0.0, yr_g = 0.0;   // the ghost of row r + 2's rate-row state (SPLIT_GHOST)
         double rb = rho_for(slb, sub, rho), rr = rho_for(slr, sur, rho);
         Res rs0 = {0, 0, 0, 0, 0, 0, 0, 0};
         int rounds = 0, ps = 0, actb = 0, actr = 0;
         double escale = 1.0;
         const double alpha = c.alpha, sig = c.sigma, dl = c.delta;
         iter = 1;
+        stamp(4, __builtin_amdgcn_s_memtime());
         while (phase != PH_DONE) {
+            if constexpr (DIAG) {   // time per phase: the previous pass of this loop went to its phase's bucket
+                const long long now = __builtin_amdgcn_s_memtime();
+                if (ph_prev == PH_POLISH) cyc_pol += now - t_prev;
+                t_prev = now;
+                ph_prev = phase;
+            }
             // ---- K = P + ks I + A' diag(kb, kr) A (row r, half h from the scratch), then the sweep: K <- -K^-1 ----
             const double kb = (phase == PH_ADMM) ? rb : (actb ? 1.0 / dl : 0.0);
             const double kr = (phase == PH_ADMM) ? rr : (actr ? 1.0 / dl : 0.0);
@@ -570,6 +606,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 double* const prow = Pg + (size_t)r * PL;
                 double o_dg = 0.0, o_sp = 0.0, o_sm = 0.0;
                 const bool has_sp = own && r + 2 < n, has_sm = own && has_prev;
+                if (SPLIT_GHOST && phase == PH_ADMM && h == 0) {   // this row's constants for the ghost update
+                    double* g = s_gh[r];
+                    g[0] = a_r; g[1] = a_rm; g[2] = slr; g[3] = sur; g[4] = rr; g[5] = 1.0 / rr;
+                }
                 if (own && h == 0) {
                     o_dg = prow[r];
                     prow[r] = o_dg + dii;
@@ -596,6 +636,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             // (= the pivot row, K symmetric) is published as two contiguous rotated slices per half, so each lane reads
             // its rotated pivot-row entries from one 16-byte aligned slice.  Pivots past n (padding) only rotate.
             bool ok = true;
+            [[maybe_unused]] const long long t_sw = DIAG ? (long long)__builtin_amdgcn_s_memtime() : 0;
             for (int hp = 0; hp < 2; ++hp) {
 #pragma unroll 2
                 for (int q = 0; q < H; ++q) {
@@ -658,6 +699,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
             for (int i = 0; i < H; ++i) Kh[i] = -Kh[i];
             __syncthreads();
+            if constexpr (DIAG) {
+                cyc_sweep += (long long)__builtin_amdgcn_s_memtime() - t_sw;
+                ++n_fact;
+            }
             if (!ok) {
                 if (phase == PH_ADMM) { status = TRAJ_STATUS_SOLVER_ERROR; break; }
                 if (c.polish_mode == 1 && rounds < c.polish_max_rounds && iter < c.max_iter) {
@@ -675,12 +720,40 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 int chk = c.check_interval - (iter - 1) % c.check_interval;
                 const double oma = 1.0 - alpha;
                 const double rib = 1.0 / rb, rir = 1.0 / rr;
+                // SPLIT_GHOST: row r also runs row r + 2's rate-row update (zr, yr: the same operations on the same
+                // values, so the same bits), which is all that A' w needs of row r + 2 -- so the iteration exchanges
+                // only xt (both neighbours in one round) and has two barriers (the broadcast, the exchange), not three.
+                const double2* const gq = reinterpret_cast<const double2*>(s_gh[r + 2]);
+                const bool has_up = own && r + 2 < n;
                 for (; iter <= c.max_iter; ++iter) {
                     const double wb = fma(rb, zb, -yb), wr = fma(rr, zr, -yr);
-                    const double rp_up = exch(a_rm * wr, +2);
+                    double rp_up;
+                    double2 g01, g23, g45;
+                    if constexpr (SPLIT_GHOST) {
+                        g01 = gq[0]; g23 = gq[1]; g45 = gq[2];   // a_r, a_rm | slr, sur | rr, 1 / rr of row r + 2
+                        rp_up = has_up ? g01.y * fma(g45.x, zr_g, -yr_g) : 0.0;
+                    } else {
+                        rp_up = exch(a_rm * wr, +2);
+                    }
                     const double atw = fma(a_b, wb, fma(a_r, wr, -rp_up));
                     const double xt = Kmul(fma(sig, x, atw - qi));
-                    const double xt_dn = exch(xt, -2);
+                    double xt_dn;
+                    if constexpr (SPLIT_GHOST) {
+                        double* buf = s_ex[xb & 3];
+                        xb++;
+                        if (h == 0) buf[r] = xt;
+                        __syncthreads();
+                        xt_dn = (own && r >= 2) ? buf[r - 2] : 0.0;
+                        const double xt_up = has_up ? buf[r + 2] : 0.0;
+                        // row r + 2's update (its xt_dn is this row's xt)
+                        const double ztr_g = fma(g01.x, xt_up, -(g01.y * xt));
+                        const double zrr_g = fma(alpha, ztr_g, oma * zr_g);
+                        const double nzr_g = clamp_mm(fma(g45.y, yr_g, zrr_g), g23.x, g23.y);
+                        yr_g = fma(g45.x, zrr_g - nzr_g, yr_g);
+                        zr_g = nzr_g;
+                    } else {
+                        xt_dn = exch(xt, -2);
+                    }
                     const double ztb = a_b * xt, ztr = fma(a_r, xt, -(a_rm * xt_dn));
                     const double xn = fma(alpha, xt, oma * x);
                     const double zrb = fma(alpha, ztb, oma * zb), zrr = fma(alpha, ztr, oma * zr);
@@ -821,6 +894,14 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 phase = PH_DONE;
             }
         }
+        if constexpr (DIAG) {
+            const long long now = __builtin_amdgcn_s_memtime();
+            if (ph_prev == PH_POLISH) cyc_pol += now - t_prev;
+            stamp(6, now);
+            stamp(5, cyc_sweep);
+            stamp(8, n_fact);
+            stamp(10, cyc_pol);
+        }
         if (iter > c.max_iter) iter = c.max_iter;
         xsol = D * x;
         if (CLOSED && a.wsWarm && t == 0) {
@@ -892,6 +973,8 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 __hip_atomic_store(&a.queue[2 + b], step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        stamp(9, iter);
+        stamp(7, __builtin_amdgcn_s_memtime());
         __syncthreads();
         continue;
     }
@@ -902,8 +985,8 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     for (int k = 0; k < N; ++k) {
         if (t < 6) {
             double v = 0.0;
-            for (int cc = 0; cc < 6; ++cc) v += gA[k * 36 + t * 6 + cc] * Xs[6 * k + cc];
-            v += gB[k * 12 + t * 2] * Ub[2 * k] + gB[k * 12 + t * 2 + 1] * Ub[2 * k + 1] + gg[6 * k + t];
+            for (int cc = 0; cc < 6; ++cc) v += gA[RA * k + t * 6 + cc] * Xs[6 * k + cc];
+            v += gB[RB * k + t * 2] * Ub[2 * k] + gB[RB * k + t * 2 + 1] * Ub[2 * k + 1] + gg[RG * k + t];
             Xs[6 * (k + 1) + t] = v;
         }
         __syncthreads();

@@ -15,19 +15,21 @@ static double* align16(double* p) {
 
 // Row-split solve for one launch of B instances (the step, the QP, one closed-loop step): H = 40 (n <= 80), 48
 // (n <= 96) or 64 (n <= 128), one workgroup of 32 rows per wave per instance
-template <int H, bool CLOSED>
+// (INLIN: the step with the linearization in the workgroup, one launch per call)
+template <int H, bool CLOSED, bool INLIN>
 static int launch_one(const KArgs& a, double* al, size_t per, hipStream_t st) {
-    hipLaunchKernelGGL((solve_split_kernel<H, CLOSED>), dim3(a.B), dim3(SplitCfg<H>::NT), 0, st, a, al, per);
+    hipLaunchKernelGGL((solve_split_kernel<H, CLOSED, false, INLIN>), dim3(a.B), dim3(SplitCfg<H>::NT), 0, st, a, al,
+                       per);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
-template <bool CLOSED>
+template <bool CLOSED, bool INLIN = false>
 static int launch_split_t(const KArgs& a, double* sws, hipStream_t st) {
     const int n = 2 * a.c.N;
     double* al = align16(sws);
     const size_t per = split_ws_doubles(a.c.N);
-    if (split_h(n) == 40) return launch_one<40, CLOSED>(a, al, per, st);
-    if (split_h(n) == 48) return launch_one<48, CLOSED>(a, al, per, st);
-    return launch_one<64, CLOSED>(a, al, per, st);
+    if (split_h(n) == 40) return launch_one<40, CLOSED, INLIN>(a, al, per, st);
+    if (split_h(n) == 48) return launch_one<48, CLOSED, INLIN>(a, al, per, st);
+    return launch_one<64, CLOSED, INLIN>(a, al, per, st);
 }
 
 // The fused closed loop (a.nsteps steps; the queue, order and lead set up by the caller): one workgroup per resident
@@ -52,11 +54,17 @@ static int launch_fused_h(const KArgs& a, double* al, size_t per, hipStream_t st
     if (G > a.B) G = a.B;
     const int minG = (a.B + TRAJ_FUSED_MAX_PER_WG - 1) / TRAJ_FUSED_MAX_PER_WG;
     if (G < minG) G = minG;
-    hipLaunchKernelGGL((solve_split_kernel<H, true, true>), dim3(G), dim3(SplitCfg<H>::NT), 0, st, a, al, per);
+    if (a.dbg)   // the stamped instance (tools/split_phase.py)
+        hipLaunchKernelGGL((solve_split_kernel<H, true, true, true, true>), dim3(G), dim3(SplitCfg<H>::NT), 0, st, a,
+                           al, per);
+    else
+        hipLaunchKernelGGL((solve_split_kernel<H, true, true>), dim3(G), dim3(SplitCfg<H>::NT), 0, st, a, al, per);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-int launch_split_step(const KArgs& a, double* sws, hipStream_t st) { return launch_split_t<false>(a, sws, st); }
+int launch_split_step(const KArgs& a, double* sws, hipStream_t st, bool inlin) {
+    return inlin ? launch_split_t<false, true>(a, sws, st) : launch_split_t<false>(a, sws, st);
+}
 int launch_split_closed(const KArgs& a, double* sws, hipStream_t st) { return launch_split_t<true>(a, sws, st); }
 int launch_split_fused(const KArgs& a, double* sws, hipStream_t st) {
     const int n = 2 * a.c.N;

@@ -269,12 +269,12 @@ static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
 
 // the row-split kernel (mpc_split.h; split_inst.hip, its own translation unit built without machine LICM like the
 // other register-resident solvers): TRAJ_MAX_N < N <= TRAJ_MAX_N_SPLIT without state bounds
-int launch_split_step(const KArgs& a, double* sws, hipStream_t st);
+int launch_split_step(const KArgs& a, double* sws, hipStream_t st, bool inlin);
 int launch_split_closed(const KArgs& a, double* sws, hipStream_t st);
 int launch_split_fused(const KArgs& a, double* sws, hipStream_t st);
 template <bool CLOSED>
 static int launch_split(const KArgs& a, double* sws, hipStream_t st) {
-    return CLOSED ? launch_split_closed(a, sws, st) : launch_split_step(a, sws, st);
+    return CLOSED ? launch_split_closed(a, sws, st) : launch_split_step(a, sws, st, false);
 }
 
 // fused run queue order: the heaviest 10 % of the instances (by the previous launch's mean ADMM
@@ -578,11 +578,14 @@ static int mpc_common(const traj_vehicle_params* p, const traj_mpc_config* c, in
     a.dbg = g_dbg;
     // the step: one launch with the linearization in the workgroup (mode 4), or rollout_kernel + jac_kernel +
     // the solve (traj_debug_step_linearize(0); the general solver always reads A/B/g from the workspace)
+    // (the row-split kernel likewise when it runs the step; the QP entry point and the other scratch solvers read A/B/g
+    // from the workspace)
     const int inlin = g_step_inlin.load(std::memory_order_relaxed);
-    if (lin && (sb || !inlin)) launch_linearize(a, (hipStream_t)stream, false);
+    const bool split_inlin = use_split && lin && inlin;
+    if (lin && ((sb && !split_inlin) || !inlin)) launch_linearize(a, (hipStream_t)stream, false);
     if (sb) {
         double* const sws = (double*)((char*)ws + base);
-        if (use_split) return launch_split<false>(a, sws, (hipStream_t)stream);
+        if (use_split) return launch_split_step(a, sws, (hipStream_t)stream, split_inlin) ? TRAJ_E_LAUNCH : TRAJ_OK;
         if (!state_bounds_active(c) && c->N <= TRAJ_MAX_N_LONG) return launch_long<false>(a, sws, (hipStream_t)stream);
         return launch_general(a, sws, (hipStream_t)stream);
     }
