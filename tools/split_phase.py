@@ -1,6 +1,6 @@
 """Per-phase cycles of the row-split kernel's fused closed loop (mpc_split.h DIAG stamps; diagnostics only).
 
-  python tools/split_phase.py [N] [kind] [steps]      (defaults: 40 mixed 20 -- config 3)
+  python tools/split_phase.py [N] [kind] [steps] [B]   (defaults: 40 mixed 20 4096 -- config 3)
 
 Runs W = 5 fused steps, then one stamped fused launch of `steps` steps (the stamped instance: solve_split_kernel with
 DIAG = true), and prints per-phase cycle statistics of each instance's last step from s_memtime stamps (one workgroup,
@@ -50,6 +50,9 @@ def main(N=40, kind="mixed", steps=20, B=4096, Ts=0.05, W=5):
         "inputs+window": d[:, 1] - d[:, 0],
         "linearization": d[:, 2] - d[:, 1],
         "condensing": d[:, 3] - d[:, 2],
+        "  condensing: sensitivities (wave 0)": d[:, 12],
+        "  condensing: products (wave 0)": d[:, 13],
+        "  condensing: barrier waits (wave 0)": d[:, 14],
         "scaling": d[:, 4] - d[:, 3],
         "solve (ADMM + sweeps + polish)": d[:, 6] - d[:, 4],
         "sweeps (every factorization)": d[:, 5],
@@ -72,4 +75,5 @@ def main(N=40, kind="mixed", steps=20, B=4096, Ts=0.05, W=5):
 
 if __name__ == "__main__":
     a = sys.argv[1:]
-    main(N=int(a[0]) if len(a) > 0 else 40, kind=a[1] if len(a) > 1 else "mixed", steps=int(a[2]) if len(a) > 2 else 20)
+    main(N=int(a[0]) if len(a) > 0 else 40, kind=a[1] if len(a) > 1 else "mixed", steps=int(a[2]) if len(a) > 2 else 20,
+         B=int(a[3]) if len(a) > 3 else 4096)

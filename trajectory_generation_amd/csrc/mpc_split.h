@@ -97,6 +97,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     __shared__ double s_xc[CLOSED || INLIN ? 6 : 1], s_uc[CLOSED || INLIN ? 2 : 1];
     __shared__ double s_prc[CLOSED ? 3 * (NR / 2 + 1) : 1];
     __shared__ double s_xs[6 * (NR / 2 + 1)];                          // outputs: X by the linear model
+    __shared__ double s_vr[NR / 2 + 1], s_sc[NR / 2 + 1][2];          // vref_k; sin / cos of the window's phi*_k
     __shared__ __attribute__((aligned(16))) double s_Fb[8][3][NRW];    // condensing: F_k rows of a block of stages
     __shared__ __attribute__((aligned(16))) double s_rec[INLIN ? LREC * (NR / 2) : 2];   // INLIN: the stage records
     __shared__ int s_item;
@@ -240,7 +241,9 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             double y, dy;
             path_eval(a.path, b, s_prc[3 * k], y, dy);
             s_prc[3 * k + 1] = y;
-            s_prc[3 * k + 2] = pm_atan(dy);
+            const double ph = pm_atan(dy);
+            s_prc[3 * k + 2] = ph;
+            pm_sincos(ph, &s_sc[k][0], &s_sc[k][1]);
         }
     }
     if constexpr (INLIN && !CLOSED) {   // the step's state and input, staged for block_linearize
@@ -250,6 +253,12 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     const double* x0 = (CLOSED || INLIN) ? s_xc : a.x0 + 6 * (size_t)b;
     const double* up = (CLOSED || INLIN) ? s_uc : a.u_prev + 2 * (size_t)b;
     const double* pref = CLOSED ? s_prc : a.path_ref + (size_t)3 * (N + 1) * b;
+    // the stage loops' per-stage inputs that do not depend on the chain, in LDS before it starts: vref_k, and sin / cos
+    // of phi*_k (one stage per thread, the same calls as in the loop)
+    for (int k = t; k <= N; k += NT) {
+        s_vr[k] = vr[k];
+        if constexpr (!CLOSED) pm_sincos(pref[3 * k + 2], &s_sc[k][0], &s_sc[k][1]);
+    }
     if (t == 0) { s_flag[0] = 0; s_flag[1] = 0; }
     __syncthreads();
     // A_k, B_k, g_k: the workspace's (stage k at gA + RA k, ...), or, fused, the stage records the workgroup's own
@@ -277,15 +286,35 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     double xh[6], G[6] = {0, 0, 0, 0, 0, 0};
     for (int i = 0; i < 6; ++i) xh[i] = x0[i];
     double qi = 0.0;
-    double Kh[H];   // row r, columns of half h: P during condensing and scaling, then K and K^-1
+    double Kh[H];   // row r, columns of half h: P after condensing, through scaling, then K and K^-1
     // The stages in blocks of KB: first the block's sensitivities -- G_k, the free response, F_k (3 values of row r per
-    // stage, published to LDS) and q -- with no row of P live, then the block's products F_k' F_k added to the half-row,
-    // which lives in registers only in that second part (between blocks it is parked in the P scratch: the two parts'
-    // registers together do not fit two waves per SIMD).  The same FMAs in the same stage order as one pass.
+    // stage, published to LDS) and q -- then the block's products on the matrix cores: P = sum_k F_k' F_k as 16 x 16
+    // tiles of the upper triangle, one v_mfma_f64_16x16x4f64 per tile and stage (k-rows = F_k's rows, one zero), the
+    // tiles dealt round-robin to the waves (accumulators in registers for the whole stage loop).  Each unordered
+    // pair of columns is formed by one accumulation, so P is exactly symmetric; F_k's columns >= 2 (k + 1) are zero
+    // (inputs of later stages), so a tile whose column block starts there adds +-0 and is skipped.  The tiles then go
+    // to the P scratch (both triangles), from which each lane loads its half-row.
     constexpr int KB = 8;
-    double* const prow_s = Pg + (size_t)r * PL + h * H;   // this lane's half-row in the scratch
+    constexpr int NB = NR / 16;                   // 16-wide column blocks
+    constexpr int NTILE = NB * (NB + 1) / 2;
+    constexpr int MT = (NTILE + WAVES - 1) / WAVES;   // tiles per wave
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    d4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+    // MFMA operand slot of this lane: k-row, column (from an opaque copy of the lane index: in the fused item loop the
+    // derived LDS / scratch addresses would otherwise be hoisted out of it and kept live across the whole solve)
+    int lane_o = lane;
+    asm volatile("" : "+v"(lane_o));
+    const int mr = (lane_o >> 4) & 3, mc = lane_o & 15;
+    // the F row in MFMA k-slot mr: F2, F1, F0, then the zero row.  v_mfma_f64_16x16x4f64 accumulates its four k-slots
+    // as one fma each, in slot order (measured: tools/split_bitcmp.py), so each entry is fma(F0, ., fma(F1, ., fma(F2,
+    // ., acc))) -- the per-lane FMA chain of the row form, bit for bit (the other slot orders differ in the last bits)
+    const int fk = mr < 3 ? 2 - mr : -1;
+    [[maybe_unused]] long long cyc_c1 = 0, cyc_c2 = 0, cyc_cb = 0, tc = 0;   // DIAG: condensing sub-phases
     for (int k0 = 0; k0 < N; k0 += KB) {
         const int kend = (k0 + KB < N) ? k0 + KB : N;
+        if constexpr (DIAG) tc = __builtin_amdgcn_s_memtime();
         for (int k = k0; k < kend; ++k) {
             const double* Ak = gA + RA * k;
             double xn[6], Gn[6];
@@ -300,11 +329,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             }
             for (int rr = 0; rr < 6; ++rr) { xh[rr] = xn[rr]; G[rr] = Gn[rr]; }
             const int k1 = k + 1;
-            double sk, ck;
-            pm_sincos(pref[3 * k1 + 2], &sk, &ck);
+            const double sk = s_sc[k1][0], ck = s_sc[k1][1];
             const double e0 = sk * (xh[0] - pref[3 * k1]) - ck * (xh[1] - pref[3 * k1 + 1]);
             const double e1 = xh[2] - pref[3 * k1 + 2];
-            const double e2 = xh[3] - vr[k1];
+            const double e2 = xh[3] - s_vr[k1];
             const double F0 = sw0 * (sk * G[0] - ck * G[1]), F1 = sw1 * G[2], F2 = sw2 * G[3];
             qi += sw0 * F0 * e0 + sw1 * F1 * e1 + sw2 * F2 * e2;
             if (h == 0) {
@@ -313,53 +341,65 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 s_Fb[k - k0][2][r] = F2;
             }
         }
+        if constexpr (DIAG) {
+            const long long now = __builtin_amdgcn_s_memtime();
+            cyc_c1 += now - tc;
+            tc = now;
+        }
         __syncthreads();
-        // the half-row back from the scratch (none before the first block); an opaque pointer, so that the compiler
-        // reloads it instead of keeping the stored values live across the sensitivity part
-        double* pp = prow_s;
-        asm volatile("" : "+v"(pp));
-        const double2* pp2 = reinterpret_cast<const double2*>(pp);
-#pragma unroll
-        for (int i = 0; i < H; i += 2) {
-            const double2 v2 = (k0 == 0) ? double2{0.0, 0.0} : pp2[i / 2];
-            Kh[i] = v2.x;
-            Kh[i + 1] = v2.y;
+        if constexpr (DIAG) {
+            const long long now = __builtin_amdgcn_s_memtime();
+            cyc_cb += now - tc;
+            tc = now;
         }
         for (int k = k0; k < kend; ++k) {
-            const double F0 = s_Fb[k - k0][0][r], F1 = s_Fb[k - k0][1][r], F2 = s_Fb[k - k0][2][r];
-            // F_k's columns >= 2 (k + 1) are zero (inputs of later stages; rows >= n hold F = 0): chunks of 8 columns
-            // from the first one that can be nonzero in half 0 (uniform skip); a half-1 lane's extra columns add zeros
-            const int jm = 2 * k + 2;
-            // (each chunk's 12 16-byte reads, then its 24 FMAs: the scheduler would otherwise issue every read first)
-            const double2* f2r[3] = {reinterpret_cast<const double2*>(&s_Fb[k - k0][0][h * H]),
-                                     reinterpret_cast<const double2*>(&s_Fb[k - k0][1][h * H]),
-                                     reinterpret_cast<const double2*>(&s_Fb[k - k0][2][h * H])};
+            double opv[NB];   // this lane's operand slot of each column block: F_k[mr][16 ib + mc] (row 3: 0)
 #pragma unroll
-            for (int c0 = 0; c0 < H; c0 += 8) {
-                if (c0 >= jm) continue;
-                double2 f0[4], f1[4], f2[4];
+            for (int ib = 0; ib < NB; ++ib) opv[ib] = (fk >= 0) ? s_Fb[k - k0][fk >= 0 ? fk : 0][16 * ib + mc] : 0.0;
+            int ti = 0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    f0[i] = f2r[0][c0 / 2 + i];
-                    f1[i] = f2r[1][c0 / 2 + i];
-                    f2[i] = f2r[2][c0 / 2 + i];
-                }
+            for (int ib = 0; ib < NB; ++ib)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    Kh[c0 + 2 * i] = fma(F0, f0[i].x, fma(F1, f1[i].x, fma(F2, f2[i].x, Kh[c0 + 2 * i])));
-                    Kh[c0 + 2 * i + 1] = fma(F0, f0[i].y, fma(F1, f1[i].y, fma(F2, f2[i].y, Kh[c0 + 2 * i + 1])));
-                }
-                __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 24, 0);
-            }
+                for (int jb = ib; jb < NB; ++jb, ++ti)
+                    if (ti % WAVES == wid && 16 * jb < 2 * k + 2)
+                        acc[ti / WAVES] = __builtin_amdgcn_mfma_f64_16x16x4f64(opv[ib], opv[jb], acc[ti / WAVES], 0, 0, 0);
         }
-        {   // park the half-row (after the last block too: the penalty band is added in the scratch, below)
-            double2* wp2 = reinterpret_cast<double2*>(pp);
-#pragma unroll
-            for (int i = 0; i < H; i += 2) wp2[i / 2] = double2{Kh[i], Kh[i + 1]};
+        if constexpr (DIAG) {
+            const long long now = __builtin_amdgcn_s_memtime();
+            cyc_c2 += now - tc;
+            tc = now;
         }
         __syncthreads();
+        if constexpr (DIAG) cyc_cb += (long long)__builtin_amdgcn_s_memtime() - tc;
     }
+    {   // the tiles to the P scratch (accumulator lane: row 16 ib + mr + 4 reg, column 16 jb + mc), both triangles;
+        // the scratch rows past NR (padding lanes' rows) are zeroed by their lanes
+        int ti = 0;
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib)
+#pragma unroll
+            for (int jb = ib; jb < NB; ++jb, ++ti)
+                if (ti % WAVES == wid) {
+#pragma unroll
+                    for (int reg = 0; reg < 4; ++reg) {
+                        const int i = 16 * ib + mr + 4 * reg, j = 16 * jb + mc;
+                        const double v = acc[ti / WAVES][reg];
+                        Pg[(size_t)i * PL + j] = v;
+                        if (ib != jb) Pg[(size_t)j * PL + i] = v;
+                    }
+                }
+        if constexpr (NRW > NR) {
+            if (r >= NR) {
+                double2* w2 = reinterpret_cast<double2*>(Pg + (size_t)r * PL + h * H);
+#pragma unroll
+                for (int i = 0; i < H; i += 2) w2[i / 2] = double2{0.0, 0.0};
+            }
+        }
+    }
+    __syncthreads();
+    stamp(12, cyc_c1);
+    stamp(13, cyc_c2);
+    stamp(14, cyc_cb);
     // input penalties U'RU and dU'Rd dU (dU_0 = U_0 - u_prev): the band of row r
     double Rs[4], Rds[4];
     Rs[0] = c.R[0]; Rs[3] = c.R[3]; Rs[1] = Rs[2] = 0.5 * (c.R[1] + c.R[2]);
@@ -384,7 +424,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();
     {
-        double* pp = prow_s;
+        double* pp = Pg + (size_t)r * PL + h * H;   // this lane's half-row
         asm volatile("" : "+v"(pp));
         const double2* pp2 = reinterpret_cast<const double2*>(pp);
 #pragma unroll
@@ -995,11 +1035,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     double op = 0.0;
     for (int k = t; k <= N; k += NT) {
         const double* X = Xs + 6 * k;
-        double s, co;
-        pm_sincos(pref[3 * k + 2], &s, &co);
+        const double s = s_sc[k][0], co = s_sc[k][1];
         const double ec = s * (X[0] - pref[3 * k]) - co * (X[1] - pref[3 * k + 1]);
         const double ep = X[2] - pref[3 * k + 2];
-        const double ev = X[3] - vr[k];
+        const double ev = X[3] - s_vr[k];
         op += c.q_c * ec * ec + c.q_phi * ep * ep + c.q_vx * ev * ev;
         if (k < N) {
             const double u0 = Ub[2 * k], u1 = Ub[2 * k + 1];
