@@ -607,11 +607,11 @@ def parse_args(argv=None):
                     help="skip the one-trajectory measurement (configs[0]: drop-in per call, fused B=1, oracle 1 thread)")
     ap.add_argument("--per-step", action="store_true",
                     help="one traj_closed_loop_step launch sequence per step instead of the fused traj_closed_loop_run")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r05.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "traffic_r06.json"),
                     help="PMC-measured HBM bytes per launch (from tools/pmc_traffic.py), if present")
-    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r05.json"),
+    ap.add_argument("--issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r06.json"),
                     help="SQ instruction counts of the fused launch (tools/pmc_f64.sh)")
-    ap.add_argument("--stall-json", default=os.path.join(HERE, "profiles", "r05_pmc_stall.json"),
+    ap.add_argument("--stall-json", default=os.path.join(HERE, "profiles", "r06_pmc_stall.json"),
                     help="SQ wave-cycle counters of the fused launch (tools/pmc_stall.sh / pmc_stall.py)")
     ap.add_argument("--knet-traffic-json", default=os.path.join(HERE, "profiles", "traffic_knet_r05.json"),
                     help="PMC-measured HBM bytes of the KalmanNet FC2 launch (tools/pmc_knet_traffic.py)")
@@ -626,8 +626,8 @@ def parse_args(argv=None):
                     help="skip the reference-semantics (cold-start) pass reported as 'cold'")
     ap.add_argument("--no-config3", dest="config3", action="store_false",
                     help="skip the configs[2] object (N = 40, mixed references, same steps / warmup; one GPU)")
-    ap.add_argument("--config3-traffic-json", default=os.path.join(HERE, "profiles", "traffic_r05_n40.json"))
-    ap.add_argument("--config3-issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r05_n40.json"))
+    ap.add_argument("--config3-traffic-json", default=os.path.join(HERE, "profiles", "traffic_r06_n40.json"))
+    ap.add_argument("--config3-issue-json", default=os.path.join(HERE, "profiles", "sq_f64_r06_n40.json"))
     ap.add_argument("--config3-stall-json", default=os.path.join(HERE, "profiles", "r06_pmc_stall_n40.json"))
     ap.add_argument("--config3-cpu-traj", type=int, default=512)
     ap.add_argument("--config3-cpu-steps", type=int, default=16)
@@ -636,7 +636,7 @@ def parse_args(argv=None):
     ap.add_argument("--dist-timeout", type=float, default=600.0,
                     help="seconds before a process-group rendezvous or collective gives up (N > 1)")
     args = ap.parse_args(argv)
-    # the profiles of another horizon (config 3's N = 40: traffic_r05_n40.json, sq_f64_r05_n40.json) when the
+    # the profiles of another horizon (config 3's N = 40: traffic_r06_n40.json, sq_f64_r06_n40.json) when the
     # defaults are in use and such a file exists
     if args.horizon != 20:
         for k in ("traffic_json", "issue_json"):

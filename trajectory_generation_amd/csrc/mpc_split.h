@@ -98,14 +98,25 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     __shared__ double s_prc[CLOSED ? 3 * (NR / 2 + 1) : 1];
     __shared__ double s_xs[6 * (NR / 2 + 1)];                          // outputs: X by the linear model
     __shared__ double s_vr[NR / 2 + 1], s_sc[NR / 2 + 1][2];          // vref_k; sin / cos of the window's phi*_k
-    __shared__ __attribute__((aligned(16))) double s_Fb[8][3][NRW];    // condensing: F_k rows of a block of stages
-    __shared__ __attribute__((aligned(16))) double s_rec[INLIN ? LREC * (NR / 2) : 2];   // INLIN: the stage records
+    // One LDS region for the condensing phase's buffers -- F_k rows of a block of stages, INLIN's stage records -- and,
+    // PLDS (the closed loop at H = 40), the scaled P after it (NR rows, stride PS): otherwise P lives in the caller's
+    // scratch, where its re-reads (each factorization, each residual check, the polish) went to HBM
+    constexpr bool PLDS = CLOSED && H == 40;
+    constexpr int PS = PLDS ? PL + 2 : PL;   // P row stride (LDS: padded against bank conflicts)
+    constexpr int UN_COND = 8 * 3 * NRW + (INLIN ? LREC * (NR / 2) : 2), UN_P = PLDS ? NR * PS : 0;
+    __shared__ __attribute__((aligned(16))) double s_un[UN_COND > UN_P ? UN_COND : UN_P];
+    double(*const s_Fb)[3][NRW] = reinterpret_cast<double(*)[3][NRW]>(s_un);   // condensing: [stage in block][F row]
+    double* const s_rec = s_un + 8 * 3 * NRW;                                     // INLIN: the stage records
     __shared__ int s_item;
     const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const int r = 32 * wid + (lane & 31), h = lane >> 5;    // row, half
     // the P scratch: per instance (one workgroup per instance), or per workgroup (fused: a workgroup solves one item
     // at a time)
-    double* const Pg = sws + (size_t)blockIdx.x * sstride;   // scaled P, row r at Pg + r PL
+    double* const Pg = sws + (size_t)blockIdx.x * sstride;   // scaled P, row r at Pg + r PL (!PLDS)
+    // row rr_ of the scaled P (PLDS: lanes past NR -- padding, never read by a real row -- alias rows below NR)
+    auto Prow = [&](int rr_) -> double* {
+        return PLDS ? s_un + (size_t)(rr_ < NR ? rr_ : rr_ - NR) * PS : Pg + (size_t)rr_ * PL;
+    };
     for (bool more = true; more;) {
     more = FUSED;
     // fused: the arguments through a pointer the compiler cannot see through, so that nothing derived from them is
@@ -384,11 +395,11 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                     for (int reg = 0; reg < 4; ++reg) {
                         const int i = 16 * ib + mr + 4 * reg, j = 16 * jb + mc;
                         const double v = acc[ti / WAVES][reg];
-                        Pg[(size_t)i * PL + j] = v;
-                        if (ib != jb) Pg[(size_t)j * PL + i] = v;
+                        Prow(i)[j] = v;
+                        if (ib != jb) Prow(j)[i] = v;
                     }
                 }
-        if constexpr (NRW > NR) {
+        if constexpr (NRW > NR && !PLDS) {
             if (r >= NR) {
                 double2* w2 = reinterpret_cast<double2*>(Pg + (size_t)r * PL + h * H);
 #pragma unroll
@@ -411,7 +422,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         // row r's band entries (columns 2 kk - 2 .. 2 kk + 3) in the scratch, by the half-0 lane (dynamic columns: no
         // per-register selects), then both halves reload the row
         if (h == 0) {
-            double* const pr_ = Pg + (size_t)r * PL;
+            double* const pr_ = Prow(r);
             const int j0 = 2 * kk - 2 > 0 ? 2 * kk - 2 : 0, j1 = 2 * kk + 4 < n ? 2 * kk + 4 : n;
             for (int j = j0; j < j1; ++j) {
                 const int kj = j >> 1;
@@ -424,7 +435,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();
     {
-        double* pp = Pg + (size_t)r * PL + h * H;   // this lane's half-row
+        double* pp = Prow(r) + h * H;   // this lane's half-row
         asm volatile("" : "+v"(pp));
         const double2* pp2 = reinterpret_cast<const double2*>(pp);
 #pragma unroll
@@ -510,11 +521,14 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         qi *= cs;
         // the scaled P to the scratch (row r's half h at Pg + r PL + h H); the padding rows r >= n hold the identity
         // row there (zero otherwise), so that K's padding pivots are trivial
-        {   // (the scratch holds NRW rows: padding rows past NR park there too, never read by a real row)
-            double2* w2 = reinterpret_cast<double2*>(Pg + (size_t)r * PL + h * H);
+        {   // (the scratch holds NRW rows: padding rows past NR park there too, never read by a real row; PLDS: they
+            // do not store)
+            if (!PLDS || r < NR) {
+                double2* w2 = reinterpret_cast<double2*>(Prow(r) + h * H);
 #pragma unroll
-            for (int i = 0; i < H; i += 2) w2[i / 2] = double2{Kh[i], Kh[i + 1]};
-            if (!own && r < NR && h == r / H) Pg[(size_t)r * PL + r] = 1.0;
+                for (int i = 0; i < H; i += 2) w2[i / 2] = double2{Kh[i], Kh[i + 1]};
+            }
+            if (!own && r < NR && h == r / H) Prow(r)[r] = 1.0;
         }
         const double csinv = 1.0 / cs;
         const double D_dn = exch(D, -2);
@@ -540,7 +554,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             const double* vb = bcast(v);
             const double2* v2 = reinterpret_cast<const double2*>(__builtin_assume_aligned(vb + h * H, 16));
             double s4[4] = {0.0, 0.0, 0.0, 0.0};
-            const double2* p2 = reinterpret_cast<const double2*>(Pg + (size_t)r * PL + h * H);
+            const double2* p2 = reinterpret_cast<const double2*>(Prow(r) + h * H);
 #pragma unroll
             for (int i0 = 0; i0 < H; i0 += 8) {
                 double2 pv[4], vv[4];
@@ -643,7 +657,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                 // The band goes into P in the scratch (row r's half-0 lane adds its diagonal and its (r, r +- 2) entries),
                 // both lanes load the row half as it stands -- no per-entry selects (their masks, invariant across the
                 // solve, are what the compiler would hoist and spill) -- and the three entries are restored.
-                double* const prow = Pg + (size_t)r * PL;
+                double* const prow = Prow(r);
                 double o_dg = 0.0, o_sp = 0.0, o_sm = 0.0;
                 const bool has_sp = own && r + 2 < n, has_sm = own && has_prev;
                 if (SPLIT_GHOST && phase == PH_ADMM && h == 0) {   // this row's constants for the ghost update
