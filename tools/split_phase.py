@@ -56,9 +56,13 @@ def main(N=40, kind="mixed", steps=20, B=4096, Ts=0.05, W=5):
         "scaling": d[:, 4] - d[:, 3],
         "solve (ADMM + sweeps + polish)": d[:, 6] - d[:, 4],
         "sweeps (every factorization)": d[:, 5],
+        "  sweeps: pivot barrier waits (wave 0)": d[:, 15],
+        "  sweeps: barrier -> reciprocal and pivot-row branch done (wave 0)": d[:, 17],
+        "  sweeps: the row update (wave 0)": d[:, 18],
         "polish pass (its sweep included)": d[:, 10],
         "admm iterations": (d[:, 6] - d[:, 4]) - d[:, 10] - sweep_per * (d[:, 8] - (d[:, 10] > 0)),
         "outputs+plant": d[:, 7] - d[:, 6],
+        "barrier waits in exchanges / broadcasts (wave 0, whole item)": d[:, 16],
         "total": d[:, 7] - d[:, 0],
     }
     it = d[:, 9]

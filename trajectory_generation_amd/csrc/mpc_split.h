@@ -169,7 +169,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     auto stamp = [&](int i, long long v) {
         if (DIAG && dbg) dbg[(size_t)b * 32 + i] = v;
     };
-    [[maybe_unused]] long long cyc_sweep = 0, cyc_pol = 0, t_prev = 0;
+    [[maybe_unused]] long long cyc_sweep = 0, cyc_pol = 0, t_prev = 0, cyc_swb = 0, cyc_xb = 0, cyc_sw1 = 0, cyc_sw2 = 0;
     [[maybe_unused]] int n_fact = 0, ph_prev = -1;
     stamp(0, __builtin_amdgcn_s_memtime());
     const traj_vehicle_params& p = a.p;
@@ -185,7 +185,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         double* buf = s_ex[xb & 3];
         xb++;
         if (h == 0) buf[r] = v;
+        [[maybe_unused]] long long tb0 = 0;
+        if constexpr (DIAG) tb0 = __builtin_amdgcn_s_memtime();
         __syncthreads();
+        if constexpr (DIAG) cyc_xb += (long long)__builtin_amdgcn_s_memtime() - tb0;
         const int s = r + delta;
         return (own && s >= 0 && s < n) ? buf[s] : 0.0;
     };
@@ -193,7 +196,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         double* buf = s_bc[bb & 1];
         bb++;
         if (h == 0) buf[r] = own ? v : 0.0;
+        [[maybe_unused]] long long tb0 = 0;
+        if constexpr (DIAG) tb0 = __builtin_amdgcn_s_memtime();
         __syncthreads();
+        if constexpr (DIAG) cyc_xb += (long long)__builtin_amdgcn_s_memtime() - tb0;
         return buf;
     };
     // Block reductions over DPP (wave_max_dpp / wave_sum_dpp: no per-lane shuffle addresses, which the compiler would
@@ -709,8 +715,18 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                     double* const sl = &s_pv[par][0][0];
                     // row r publishes its K[r][p] = K[p][r] at slice position (r mod H) and (r mod H) + H of half r / H
                     if (r < NR) sl[(r / H) * SPV + off + (r % H) + h * H] = kp;
+                    [[maybe_unused]] long long ts0 = 0;
+                    if constexpr (DIAG) ts0 = __builtin_amdgcn_s_memtime();
                     __syncthreads();
+                    if constexpr (DIAG) cyc_swb += (long long)__builtin_amdgcn_s_memtime() - ts0;
                     const double d = sl[hp * SPV + off + q];
+                    // rotated pivot-row entries of this half: K[p][h H + (i + q) mod H] at sl[h SPV + off + q + i] --
+                    // the first chunk read with d, ahead of the reciprocal and the pivot row's branch
+                    const double2* pr2 =
+                        reinterpret_cast<const double2*>(__builtin_assume_aligned(sl + h * SPV + off + q, 16));
+                    double2 cur[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cur[i] = pr2[i];
                     ok = ok && (d > 0.0);
                     const double dinv = rcp_nr(d);
                     const bool piv = (r == pv);
@@ -721,12 +737,11 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
                         for (int i = 0; i < H; ++i) Kh[i] = 0.0;
                     }
-                    // rotated pivot-row entries of this half: K[p][h H + (i + q) mod H] at sl[h SPV + off + q + i]
-                    const double2* pr2 =
-                        reinterpret_cast<const double2*>(__builtin_assume_aligned(sl + h * SPV + off + q, 16));
-                    double2 cur[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) cur[i] = pr2[i];
+                    [[maybe_unused]] long long ts2 = 0;
+                    if constexpr (DIAG) {
+                        ts2 = __builtin_amdgcn_s_memtime();
+                        cyc_sw1 += ts2 - ts0;
+                    }
                     const double last = fma3(be, cur[0].x, Kh[0]);   // column h H + q (the non-pivot half's entry)
 #pragma unroll
                     for (int i0 = 0; i0 < H; i0 += 8) {
@@ -748,6 +763,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                         }
                     }
                     Kh[H - 1] = (h == hp) ? k0 : last;
+                    if constexpr (DIAG) cyc_sw2 += (long long)__builtin_amdgcn_s_memtime() - ts2;
                 }
             }
 #pragma unroll
@@ -955,6 +971,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             stamp(5, cyc_sweep);
             stamp(8, n_fact);
             stamp(10, cyc_pol);
+            stamp(15, cyc_swb);
+            stamp(16, cyc_xb);
+            stamp(17, cyc_sw1);
+            stamp(18, cyc_sw2);
         }
         if (iter > c.max_iter) iter = c.max_iter;
         xsol = D * x;
