@@ -423,17 +423,22 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     Rds[0] = c.Rd[0]; Rds[3] = c.Rd[3]; Rds[1] = Rds[2] = 0.5 * (c.Rd[1] + c.Rd[2]);
     const double Rs0 = ch ? Rs[2] : Rs[0], Rs1 = ch ? Rs[3] : Rs[1];
     const double Rd0 = ch ? Rds[2] : Rds[0], Rd1 = ch ? Rds[3] : Rds[1];
-    const double dmul = (kk < N - 1) ? 2.0 : 1.0;
     if (own) {
         // row r's band entries (columns 2 kk - 2 .. 2 kk + 3) in the scratch, by the half-0 lane (dynamic columns: no
         // per-register selects), then both halves reload the row
         if (h == 0) {
-            double* const pr_ = Prow(r);
-            const int j0 = 2 * kk - 2 > 0 ? 2 * kk - 2 : 0, j1 = 2 * kk + 4 < n ? 2 * kk + 4 : n;
+            // (from an opaque copy of the row index: the band's row address, formed once outside the fused item loop,
+            // would stay live across it and spill)
+            int r_o = r;
+            asm volatile("" : "+v"(r_o));
+            const int kk_o = r_o >> 1;
+            const double dmul = (kk_o < N - 1) ? 2.0 : 1.0;
+            double* const pr_ = Prow(r_o);
+            const int j0 = 2 * kk_o - 2 > 0 ? 2 * kk_o - 2 : 0, j1 = 2 * kk_o + 4 < n ? 2 * kk_o + 4 : n;
             for (int j = j0; j < j1; ++j) {
                 const int kj = j >> 1;
                 const double rs = (j & 1) ? Rs1 : Rs0, rd = (j & 1) ? Rd1 : Rd0;
-                const double add = (kj == kk) ? 2.0 * rs + 2.0 * rd * dmul : -2.0 * rd;
+                const double add = (kj == kk_o) ? 2.0 * rs + 2.0 * rd * dmul : -2.0 * rd;
                 pr_[j] = pr_[j] + add;
             }
         }
@@ -733,7 +738,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                     const double fd = kp * dinv;
                     const double be = piv ? dinv : -fd;
                     const double k0 = piv ? -dinv : fd;
-                    if (piv) {   // the pivot row becomes K_pj / d: an exact zero row plus be * K_pj
+#ifndef TGMPC_SPLIT_NOZERO_TIMING
+#define TGMPC_SPLIT_NOZERO_TIMING 0   // 1: timing experiment only (wrong results): the pivot row is not zeroed
+#endif
+                    if (piv && !TGMPC_SPLIT_NOZERO_TIMING) {   // the pivot row becomes K_pj / d: an exact zero row plus be * K_pj
 #pragma unroll
                         for (int i = 0; i < H; ++i) Kh[i] = 0.0;
                     }
