@@ -3,10 +3,10 @@
   python tools/split_probe.py [N,N,...]
 
 Per N: (1) the batch step entry point (traj_mpc_step_batch) at B = 1024 and 4096 on random parabola windows (dt 0.05)
-with the default routing (capacity 80: one launch, linearization in the kernel) and with the row-split kernel
-(traj_debug_split_min_n: rollout_kernel + jac_kernel + solve_split_kernel) -- time per call, statuses and u agreement;
-(2) config 3's closed loop (4096 mixed references, N = 40, dt 0.05, 20 steps after 5 warmup): the fused capacity-80
-launch (the bench path) against per-step launch sequences on the row-split kernel, and per-step on capacity 80.
+on the capacity-80 kernel (traj_debug_split_min_n(41)) and on the row-split kernel (the default since round 6:
+traj_debug_split_min_n(21)) -- time per call, statuses and u agreement; (2) config 3's closed loop (4096 mixed
+references, N = 40, dt 0.05, 20 steps after 5 warmup): the fused launch on each kernel, and per-step launches on the
+row-split kernel; (3) one instance at the 10,000-iteration cap re-solved alone on each (per-iteration latency).
 One JSON line per measurement."""
 import json
 import sys
