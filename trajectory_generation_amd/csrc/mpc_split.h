@@ -192,6 +192,20 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         const int s = r + delta;
         return (own && s >= 0 && s < n) ? buf[s] : 0.0;
     };
+    // two exchanges in one round (one barrier): the values of rows r + d1 and r + d2
+    auto exch2 = [&](double v1, int d1, double v2, int d2, double& o1, double& o2) {
+        double* buf1 = s_ex[xb & 3];
+        double* buf2 = s_ex[(xb + 1) & 3];
+        xb += 2;
+        if (h == 0) {
+            buf1[r] = v1;
+            buf2[r] = v2;
+        }
+        __syncthreads();
+        const int s1 = r + d1, s2 = r + d2;
+        o1 = (own && s1 >= 0 && s1 < n) ? buf1[s1] : 0.0;
+        o2 = (own && s2 >= 0 && s2 < n) ? buf2[s2] : 0.0;
+    };
     auto bcast = [&](double v) -> const double* {
         double* buf = s_bc[bb & 1];
         bb++;
@@ -224,15 +238,24 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         }
         __syncthreads();
     };
-    // block sum of the rows' values (half-0 lanes) in a fixed order: the DPP pattern per wave, then the waves in order
-    auto block_sum = [&](double v) -> double {
-        v = wave_sum_dpp((h == 0) ? v : 0.0);
-        if (lane == 0) s_red[wid * 8] = v;
+    // block sum of sv over the rows (half-0 lanes: the DPP pattern per wave, then the waves in order) and block max of
+    // mv, in one round
+    auto block_sum_max = [&](double sv, double mv, double& so, double& mo) {
+        sv = wave_sum_dpp((h == 0) ? sv : 0.0);
+        double m1[1] = {mv};
+        wave_max_dpp<1>(m1);
+        if (lane == 0) {
+            s_red[wid * 8] = sv;
+            s_red[wid * 8 + 1] = m1[0];
+        }
         __syncthreads();
-        double s = 0.0;
-        for (int w = 0; w < WAVES; ++w) s += s_red[w * 8];
+        double sacc = 0.0;
+        for (int w = 0; w < WAVES; ++w) sacc += s_red[w * 8];
+        double m = s_red[1];
+        for (int w = 1; w < WAVES; ++w) m = nmax(m, s_red[w * 8 + 1]);
         __syncthreads();
-        return s;
+        so = sacc;
+        mo = m;
     };
 
     // ---- inputs (:144-163 normalisation by the caller; CLOSED: state, u_prev and the window) ----
@@ -312,6 +335,30 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     // (inputs of later stages), so a tile whose column block starts there adds +-0 and is skipped.  The tiles then go
     // to the P scratch (both triangles), from which each lane loads its half-row.
     constexpr int KB = 8;
+    // Row rr of A_k x (+ v) as the chain v = fma(A[rr][cc], x[cc], v), cc = 0..5.  CLOSED: A_k comes from the library's
+    // own linearization, whose structural entries are exact (f does not read X, Y; f_0, f_1 do not read omega;
+    // f_2 = omega; f_3..5 do not read phi: rows 0 / 1 = [1 0 a a a 0], row 2 = [0 0 1 0 0 a], rows 3..5 =
+    // [0 0 0 a a a]), so the chain skips the zero terms and adds the unit ones -- the values of the full chain (up to
+    // the sign of a zero), as mpc_solve.h's capacity kernels form them; the step entry point keeps the full chain.
+    auto arow = [&](const double* Ak, int rr, const double* x, double v) -> double {
+        if constexpr (CLOSED) {
+            if (rr <= 1) {
+                v = v + x[rr];
+#pragma unroll
+                for (int cc = 2; cc < 5; ++cc) v = fma(Ak[6 * rr + cc], x[cc], v);
+            } else if (rr == 2) {
+                v = v + x[2];
+                v = fma(Ak[6 * 2 + 5], x[5], v);
+            } else {
+#pragma unroll
+                for (int cc = 3; cc < 6; ++cc) v = fma(Ak[6 * rr + cc], x[cc], v);
+            }
+        } else {
+#pragma unroll
+            for (int cc = 0; cc < 6; ++cc) v = fma(Ak[6 * rr + cc], x[cc], v);
+        }
+        return v;
+    };
     constexpr int NB = NR / 16;                   // 16-wide column blocks
     constexpr int NTILE = NB * (NB + 1) / 2;
     constexpr int MT = (NTILE + WAVES - 1) / WAVES;   // tiles per wave
@@ -336,12 +383,8 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             const double* Ak = gA + RA * k;
             double xn[6], Gn[6];
             for (int rr = 0; rr < 6; ++rr) {
-                double v = gg[RG * k + rr], w = 0.0;
-                for (int cc = 0; cc < 6; ++cc) {
-                    v = fma(Ak[6 * rr + cc], xh[cc], v);
-                    w = fma(Ak[6 * rr + cc], G[cc], w);
-                }
-                xn[rr] = v;
+                xn[rr] = arow(Ak, rr, xh, gg[RG * k + rr]);
+                const double w = arow(Ak, rr, G, 0.0);
                 Gn[rr] = (own && kk == k) ? gB[RB * k + 2 * rr + ch] : w;
             }
             for (int rr = 0; rr < 6; ++rr) { xh[rr] = xn[rr]; G[rr] = Gn[rr]; }
@@ -500,7 +543,8 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
         double D = 1.0, Eb = 1.0, Er = 1.0, cs = 1.0, cn = 0.0;
         cn = own ? row_absmax() : 0.0;
         for (int it = 0; it < c.scaling_iters; ++it) {
-            const double Er_up = exch(Er, +2), D_dn = exch(D, -2);
+            double Er_up, D_dn;
+            exch2(Er, +2, D, -2, Er_up, D_dn);
             const double a_b = Eb * D, a_r = Er * D, a_rm = has_prev ? Er * D_dn : 0.0, a_rp = Er_up * D;
             const double pn = cs * cn;
             const double coln = fmax(pn, fmax(fmax(fabs(a_b), fabs(a_r)), fabs(a_rp)));
@@ -520,10 +564,10 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             D *= Dt;
             Eb *= Etb;
             Er *= Etr;
-            const double mean = block_sum(own ? cs * cn : 0.0) / n;
-            double qv[1] = {own ? fabs(cs * qi) : 0.0};
-            block_max(qv);
-            double ct = fmax(mean, limit_scaling(qv[0]));
+            double csum, qmax;
+            block_sum_max(own ? cs * cn : 0.0, own ? fabs(cs * qi) : 0.0, csum, qmax);
+            const double mean = csum / n;
+            double ct = fmax(mean, limit_scaling(qmax));
             ct = 1.0 / limit_scaling(ct);
             cs *= ct;
         }
