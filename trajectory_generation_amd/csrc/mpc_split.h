@@ -76,6 +76,13 @@ __device__ __forceinline__ double pair_max(double v) {   // NaN-propagating
 #define TGMPC_SPLIT_GHOST 1
 #endif
 constexpr bool SPLIT_GHOST = TGMPC_SPLIT_GHOST != 0;
+#ifndef TGMPC_SPLIT_BLOCK2
+#define TGMPC_SPLIT_BLOCK2 1   // the sweep takes its pivots two at a time (one LDS round and one barrier per pair)
+#endif
+constexpr bool SPLIT_BLOCK2 = TGMPC_SPLIT_BLOCK2 != 0;
+#ifndef TGMPC_SPLIT_NOZERO_TIMING
+#define TGMPC_SPLIT_NOZERO_TIMING 0   // 1: timing experiment only (wrong results): the pivot rows are not zeroed
+#endif
 // DIAG (fused only, when a diagnostic buffer is set: traj_debug_set_stamps): per-phase s_memtime stamps of each
 // instance's last step in a.dbg[b][0..11] (tools/split_phase.py); the production instances compile none of it.
 template <int H, bool CLOSED = false, bool FUSED = false, bool INLIN = FUSED, bool DIAG = false>
@@ -91,7 +98,8 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     __shared__ double s_ex[4][NRW];                                    // +-2 exchanges (rotating)
     // ADMM: every row's constants of the rate-row update, read by the row two below it (the ghost update, below)
     __shared__ __attribute__((aligned(16))) double s_gh[SPLIT_GHOST ? NRW + 2 : 1][6];
-    __shared__ __attribute__((aligned(16))) double s_pv[2][2][SPV];    // sweep: [pivot parity][half][slice]
+    __shared__ __attribute__((aligned(16))) double s_pv[SPLIT_BLOCK2 ? 1 : 2][2][SPV];   // sweep: [parity][half][slice]
+    __shared__ __attribute__((aligned(16))) double s_pv2[SPLIT_BLOCK2 ? 2 : 1][2][2][SPV];  // block sweep: [parity][col][half][slice]
     __shared__ double s_red[WAVES * 8];
     __shared__ int s_flag[4];
     __shared__ double s_xc[CLOSED || INLIN ? 6 : 1], s_uc[CLOSED || INLIN ? 2 : 1];
@@ -746,6 +754,106 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
             // its rotated pivot-row entries from one 16-byte aligned slice.  Pivots past n (padding) only rotate.
             bool ok = true;
             [[maybe_unused]] const long long t_sw = DIAG ? (long long)__builtin_amdgcn_s_memtime() : 0;
+            // SPLIT_BLOCK2: pivots p, p + 1 (q even, both in half hp: H and n are even) as one 2 x 2 block -- the
+            // composition of the two single sweeps, with the second pivot's d and every coefficient formed as the
+            // sequential sweep forms them (a = K_pp, b = K_p+1,p, c = K_p+1,p+1; 1/a; d2 = c - (b/a) b; 1/d2):
+            //   row r outside the block: u = K_rp, v = K_r,p+1; beta = (v - (u/a) b)/d2, alpha = (u - beta b)/a;
+            //     K_rj <- K_rj - alpha K_pj - beta K_p+1,j, and (K_rp, K_r,p+1) <- (alpha, beta);
+            //   rows p, p + 1: the rows of the block inverse G (g00 = 1/a + (b/a)^2/d2, g01 = g10 = -(b/a)/d2,
+            //     g11 = 1/d2) times the pivot rows, from an exact zero row, and (K_pp .. ) <- -G.
+            // The two pivot columns are published as two slices (A: column p, B: column p + 1) in the rotated layout
+            // of the single sweep; registers rotate by two per block.  The same algebra as two single pivots, one
+            // barrier and one LDS round instead of two; the rounding of the composed coefficients differs in the
+            // last bits from the sequential form.
+            if constexpr (SPLIT_BLOCK2) {
+                for (int hp = 0; hp < 2; ++hp) {
+#pragma unroll 2
+                    for (int q = 0; q < H; q += 2) {
+                        const int pv = hp * H + q;
+                        if (pv >= n) {   // a padding pair: identity rows, a rotation by two only
+                            const double k0 = Kh[0], k1 = Kh[1];
+#pragma unroll
+                            for (int i = 2; i < H; ++i) Kh[i - 2] = Kh[i];
+                            Kh[H - 2] = k0;
+                            Kh[H - 1] = k1;
+                            continue;
+                        }
+                        double e0, e1, f0, f1;
+                        swap32(Kh[0], e0, e1);
+                        swap32(Kh[1], f0, f1);
+                        const double u = hp ? e1 : e0;   // K[r][p]
+                        const double v = hp ? f1 : f0;   // K[r][p + 1]
+                        const int par = (pv >> 1) & 1;
+                        double* const slA = &s_pv2[par][0][0][0];
+                        double* const slB = &s_pv2[par][1][0][0];
+                        if (r < NR) {
+                            slA[(r / H) * SPV + (r % H) + h * H] = u;
+                            slB[(r / H) * SPV + (r % H) + h * H] = v;
+                        }
+                        [[maybe_unused]] long long ts0 = 0;
+                        if constexpr (DIAG) ts0 = __builtin_amdgcn_s_memtime();
+                        __syncthreads();
+                        if constexpr (DIAG) cyc_swb += (long long)__builtin_amdgcn_s_memtime() - ts0;
+                        const double2 ab = *reinterpret_cast<const double2*>(&slA[hp * SPV + q]);   // K_pp, K_p+1,p
+                        const double cc = slB[hp * SPV + q + 1];                                     // K_p+1,p+1
+                        // the pivot rows' entries of this half, rotated: K[p | p + 1][h H + (i + q) mod H]
+                        const double2* pa2 =
+                            reinterpret_cast<const double2*>(__builtin_assume_aligned(slA + h * SPV + q, 16));
+                        const double2* pb2 =
+                            reinterpret_cast<const double2*>(__builtin_assume_aligned(slB + h * SPV + q, 16));
+                        double2 ca[2], cb[2];
+#pragma unroll
+                        for (int i = 0; i < 2; ++i) {
+                            ca[i] = pa2[i];
+                            cb[i] = pb2[i];
+                        }
+                        const double a = ab.x, bb = ab.y;
+                        const double ainv = rcp_nr(a);
+                        const double t = bb * ainv;
+                        const double d2 = fma(-t, bb, cc);
+                        ok = ok && (a > 0.0) && (d2 > 0.0);
+                        const double d2inv = rcp_nr(d2);
+                        const bool p0 = (r == pv), p1 = (r == pv + 1);
+                        const double td = t * d2inv;
+                        const double beta = fma(-(u * ainv), bb, v) * d2inv;
+                        const double alpha = fma(-beta, bb, u) * ainv;
+                        // coefficients of the two pivot rows: -(alpha, beta) outside the block, G's row inside
+                        const double cA = p0 ? fma(td, t, ainv) : (p1 ? -td : -alpha);
+                        const double cB = p0 ? -td : (p1 ? d2inv : -beta);
+                        if ((p0 || p1) && !TGMPC_SPLIT_NOZERO_TIMING) {
+#pragma unroll
+                            for (int i = 0; i < H; ++i) Kh[i] = 0.0;
+                        }
+                        [[maybe_unused]] long long ts2 = 0;
+                        if constexpr (DIAG) {
+                            ts2 = __builtin_amdgcn_s_memtime();
+                            cyc_sw1 += ts2 - ts0;
+                        }
+                        // old registers 0, 1 (the pivot columns in half hp, ordinary columns in the other half)
+                        const double w0 = fma3(cA, ca[0].x, fma(cB, cb[0].x, Kh[0]));
+                        const double w1 = fma3(cA, ca[0].y, fma(cB, cb[0].y, Kh[1]));
+                        Kh[0] = fma3(cA, ca[1].x, fma(cB, cb[1].x, Kh[2]));
+                        Kh[1] = fma3(cA, ca[1].y, fma(cB, cb[1].y, Kh[3]));
+#pragma unroll
+                        for (int c4 = 4; c4 < H; c4 += 4) {   // columns c4 .. c4 + 3 (double2 c4 / 2, c4 / 2 + 1)
+#pragma unroll
+                            for (int i = 0; i < 2; ++i) {
+                                ca[i] = pa2[c4 / 2 + i];
+                                cb[i] = pb2[c4 / 2 + i];
+                            }
+#pragma unroll
+                            for (int i = 0; i < 2; ++i) {
+                                const int j = c4 + 2 * i;
+                                Kh[j - 2] = fma3(cA, ca[i].x, fma(cB, cb[i].x, Kh[j]));
+                                Kh[j - 1] = fma3(cA, ca[i].y, fma(cB, cb[i].y, Kh[j + 1]));
+                            }
+                        }
+                        Kh[H - 2] = (h == hp) ? -cA : w0;
+                        Kh[H - 1] = (h == hp) ? -cB : w1;
+                        if constexpr (DIAG) cyc_sw2 += (long long)__builtin_amdgcn_s_memtime() - ts2;
+                    }
+                }
+            } else
             for (int hp = 0; hp < 2; ++hp) {
 #pragma unroll 2
                 for (int q = 0; q < H; ++q) {
@@ -782,9 +890,6 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                     const double fd = kp * dinv;
                     const double be = piv ? dinv : -fd;
                     const double k0 = piv ? -dinv : fd;
-#ifndef TGMPC_SPLIT_NOZERO_TIMING
-#define TGMPC_SPLIT_NOZERO_TIMING 0   // 1: timing experiment only (wrong results): the pivot row is not zeroed
-#endif
                     if (piv && !TGMPC_SPLIT_NOZERO_TIMING) {   // the pivot row becomes K_pj / d: an exact zero row plus be * K_pj
 #pragma unroll
                         for (int i = 0; i < H; ++i) Kh[i] = 0.0;
