@@ -77,11 +77,14 @@ __device__ __forceinline__ double pair_max(double v) {   // NaN-propagating
 #endif
 constexpr bool SPLIT_GHOST = TGMPC_SPLIT_GHOST != 0;
 #ifndef TGMPC_SPLIT_BLOCK
-#define TGMPC_SPLIT_BLOCK 2   // pivots per sweep round (1, 2 or 4): one LDS round and one barrier per block
+// pivots per sweep round: 2 (one LDS round and one barrier per pair; the default) or 1 (the single sweep).  A 4-pivot
+// form (a per-lane LDL' solve of the block) measured 1.34-1.37 M against 1.42 M at config 3 and moved one capped
+// instance's status in test_config3_iteration_cap_steps_vs_oracle; it is not kept
+#define TGMPC_SPLIT_BLOCK 2
 #endif
 constexpr int SPLIT_BLOCK = TGMPC_SPLIT_BLOCK;
 constexpr bool SPLIT_BLOCK2 = SPLIT_BLOCK == 2;
-static_assert(SPLIT_BLOCK == 1 || SPLIT_BLOCK == 2 || SPLIT_BLOCK == 4, "sweep block");
+static_assert(SPLIT_BLOCK == 1 || SPLIT_BLOCK == 2, "sweep block");
 #ifndef TGMPC_SPLIT_NOZERO_TIMING
 #define TGMPC_SPLIT_NOZERO_TIMING 0   // 1: timing experiment only (wrong results): the pivot rows are not zeroed
 #endif
@@ -102,7 +105,7 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
     __shared__ __attribute__((aligned(16))) double s_gh[SPLIT_GHOST ? NRW + 2 : 1][6];
     __shared__ __attribute__((aligned(16))) double s_pv[SPLIT_BLOCK > 1 ? 1 : 2][2][SPV];   // sweep: [parity][half][slice]
     // block sweep: [parity][column of the block][half][slice]
-    __shared__ __attribute__((aligned(16))) double s_pv2[SPLIT_BLOCK > 1 ? 2 : 1][SPLIT_BLOCK > 1 ? SPLIT_BLOCK : 1][2][SPV];
+    __shared__ __attribute__((aligned(16))) double s_pv2[SPLIT_BLOCK2 ? 2 : 1][SPLIT_BLOCK2 ? 2 : 1][2][SPV];
     __shared__ double s_red[WAVES * 8];
     __shared__ int s_flag[4];
     __shared__ double s_xc[CLOSED || INLIN ? 6 : 1], s_uc[CLOSED || INLIN ? 2 : 1];
@@ -853,123 +856,6 @@ __global__ __launch_bounds__(SplitCfg<H>::NT) __attribute__((amdgpu_waves_per_eu
                         }
                         Kh[H - 2] = (h == hp) ? -cA : w0;
                         Kh[H - 1] = (h == hp) ? -cB : w1;
-                        if constexpr (DIAG) cyc_sw2 += (long long)__builtin_amdgcn_s_memtime() - ts2;
-                    }
-                }
-            } else if constexpr (SPLIT_BLOCK == 4) {
-                // SPLIT_BLOCK = 4: pivots p .. p + 3 (q a multiple of 4, one half; a block past n is padding, a
-                // block that reaches past n holds identity padding pivots, which couple to nothing).  Every lane
-                // forms the block's LDL' in the sequential sweep's order (uniform values), then its coefficient
-                // vector w = D^-1 z: z = -u (u = K[r][P]) outside the block, z = e_k on pivot row p + k; row r
-                // <- row r + sum_k w_k K[p + k][.] (from an exact zero row on the pivot rows), K[r][P] <- -w.
-                constexpr int M = 4;
-                for (int hp = 0; hp < 2; ++hp) {
-#pragma unroll 1
-                    for (int q = 0; q < H; q += M) {
-                        const int pv = hp * H + q;
-                        if (pv >= n) {   // a padding block: a rotation by M only
-                            double k4[M];
-#pragma unroll
-                            for (int i = 0; i < M; ++i) k4[i] = Kh[i];
-#pragma unroll
-                            for (int i = M; i < H; ++i) Kh[i - M] = Kh[i];
-#pragma unroll
-                            for (int i = 0; i < M; ++i) Kh[H - M + i] = k4[i];
-                            continue;
-                        }
-                        double u[M];
-#pragma unroll
-                        for (int i = 0; i < M; ++i) {
-                            double e0, e1;
-                            swap32(Kh[i], e0, e1);
-                            u[i] = hp ? e1 : e0;   // K[r][p + i]
-                        }
-                        const int par = (pv / M) & 1;
-                        if (r < NR) {
-#pragma unroll
-                            for (int i = 0; i < M; ++i) s_pv2[par][i][0][(r / H) * SPV + (r % H) + h * H] = u[i];
-                        }
-                        [[maybe_unused]] long long ts0 = 0;
-                        if constexpr (DIAG) ts0 = __builtin_amdgcn_s_memtime();
-                        __syncthreads();
-                        if constexpr (DIAG) cyc_swb += (long long)__builtin_amdgcn_s_memtime() - ts0;
-                        // the block, lower triangle: D[i][k] = K[p + i][p + k] = slice k at position q + i of half hp
-                        double Dl[M][M];
-#pragma unroll
-                        for (int k = 0; k < M; ++k)
-#pragma unroll
-                            for (int i = k; i < M; ++i) Dl[i][k] = s_pv2[par][k][hp][q + i];
-                        const double2* pr2[M];
-#pragma unroll
-                        for (int k = 0; k < M; ++k)
-                            pr2[k] = reinterpret_cast<const double2*>(__builtin_assume_aligned(&s_pv2[par][k][h][q], 16));
-                        double2 cs[M][2];   // the current chunk of 4 columns of each pivot row
-#pragma unroll
-                        for (int k = 0; k < M; ++k) {
-                            cs[k][0] = pr2[k][0];
-                            cs[k][1] = pr2[k][1];
-                        }
-                        // LDL' of the block, as the sequential sweep eliminates it
-                        double dinv[M], Lm[M][M];
-#pragma unroll
-                        for (int k = 0; k < M; ++k) {
-                            ok = ok && (Dl[k][k] > 0.0);
-                            dinv[k] = rcp_nr(Dl[k][k]);
-#pragma unroll
-                            for (int i = k + 1; i < M; ++i) {
-                                Lm[i][k] = Dl[i][k] * dinv[k];
-#pragma unroll
-                                for (int j = k + 1; j <= i; ++j) Dl[i][j] = fma(-Lm[i][k], Dl[j][k], Dl[i][j]);
-                            }
-                        }
-                        const int kp = r - pv;
-                        const bool inblk = (kp >= 0 && kp < M);
-                        double w[M];
-#pragma unroll
-                        for (int i = 0; i < M; ++i) w[i] = inblk ? (i == kp ? 1.0 : 0.0) : -u[i];
-#pragma unroll
-                        for (int k = 0; k < M; ++k)
-#pragma unroll
-                            for (int i = k + 1; i < M; ++i) w[i] = fma(-Lm[i][k], w[k], w[i]);
-#pragma unroll
-                        for (int k = 0; k < M; ++k) w[k] *= dinv[k];
-#pragma unroll
-                        for (int k = M - 1; k >= 0; --k)
-#pragma unroll
-                            for (int i = k + 1; i < M; ++i) w[k] = fma(-Lm[i][k], w[i], w[k]);
-                        if (inblk && !TGMPC_SPLIT_NOZERO_TIMING) {
-#pragma unroll
-                            for (int i = 0; i < H; ++i) Kh[i] = 0.0;
-                        }
-                        [[maybe_unused]] long long ts2 = 0;
-                        if constexpr (DIAG) {
-                            ts2 = __builtin_amdgcn_s_memtime();
-                            cyc_sw1 += ts2 - ts0;
-                        }
-                        // column c of the current chunk: Kh + sum_k w_k K[p + k][column]
-                        auto upd = [&](int c, double kv) -> double {
-                            const double s0 = (c & 1) ? cs[0][c >> 1].y : cs[0][c >> 1].x;
-                            const double s1 = (c & 1) ? cs[1][c >> 1].y : cs[1][c >> 1].x;
-                            const double s2 = (c & 1) ? cs[2][c >> 1].y : cs[2][c >> 1].x;
-                            const double s3 = (c & 1) ? cs[3][c >> 1].y : cs[3][c >> 1].x;
-                            return fma3(w[0], s0, fma(w[1], s1, fma(w[2], s2, fma(w[3], s3, kv))));
-                        };
-                        // old registers 0..3 (the block's columns in half hp, ordinary columns in the other half)
-                        double wl[M];
-#pragma unroll
-                        for (int c = 0; c < M; ++c) wl[c] = upd(c, Kh[c]);
-#pragma unroll
-                        for (int c4 = 4; c4 < H; c4 += 4) {
-#pragma unroll
-                            for (int k = 0; k < M; ++k) {
-                                cs[k][0] = pr2[k][c4 / 2];
-                                cs[k][1] = pr2[k][c4 / 2 + 1];
-                            }
-#pragma unroll
-                            for (int c = 0; c < 4; ++c) Kh[c4 + c - M] = upd(c, Kh[c4 + c]);
-                        }
-#pragma unroll
-                        for (int c = 0; c < M; ++c) Kh[H - M + c] = (h == hp) ? -w[c] : wl[c];
                         if constexpr (DIAG) cyc_sw2 += (long long)__builtin_amdgcn_s_memtime() - ts2;
                     }
                 }
