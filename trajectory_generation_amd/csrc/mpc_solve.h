@@ -69,6 +69,14 @@
 #ifndef TGMPC_SWEEP_UNROLL2
 #define TGMPC_SWEEP_UNROLL2 4  // two-wave sweep (capacity 80): the same
 #endif
+#ifndef TGMPC_SWEEP_PAIR
+#define TGMPC_SWEEP_PAIR 0     // one-wave sweep: pivots in 2 x 2 blocks (one barrier and one LDS round per pair; 0: single).
+                               // Round 6: all 133 GPU tests green with it, but 200 steps 16.0 M against 16.1 M single
+                               // (20 steps within noise, +20 B/lane scratch): off -- same instructions per pivot
+#endif
+#ifndef TGMPC_PAIR_CH
+#define TGMPC_PAIR_CH 4        // one-wave pair sweep: pivot-row entries (double2 of the two rows) per chunk
+#endif
 #define TGMPC_PRAGMA_(x) _Pragma(#x)
 #define TGMPC_PRAGMA(x) TGMPC_PRAGMA_(x)
 #ifndef TGMPC_RECV2
@@ -208,7 +216,8 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
     // two waves 3 fixed slots (4, 5, 6) for the ADMM loop's three exchanges, so no rotating index lives
     // across that loop (at NN = 80 it was spilled and reloaded from scratch in every exchange)
     constexpr int NEX = (WAVES > 1) ? (4 * NN + 3 * NT > 6 * NN ? 4 * NN + 3 * NT : 6 * NN) : (CMP ? 4 * NN : 6 * NN);
-    constexpr int NSW = 2 * (2 * NN + 2);
+    // sweep pivot columns: 2 slots of 2 NN + 2 doubles (single pivots), or of 2 NN double2 (one-wave pair sweep)
+    constexpr int NSW = (WAVES == 1 && TGMPC_SWEEP_PAIR) ? 8 * NN : 2 * (2 * NN + 2);
     constexpr int FS = 16 * ((NN + 15) / 16);
     constexpr int NFS = (WAVES > 1) ? 0 : (CMP ? 1 : 2) * 4 * FS;   // condensing F_k rows: slots of 4 x FS (one wave)
     // CMP: one scratch region for the exchange / broadcast slots (ADMM, Ruiz, polish), the sweep's pivot
@@ -1448,7 +1457,105 @@ __global__ __launch_bounds__(((NN + 63) / 64) * 64) __attribute__((amdgpu_waves_
 #if TGMPC_PRIO_SWEEP
             if (FUSED) __builtin_amdgcn_s_setprio(2);   // the sweep's pivot chain is LDS-latency bound
 #endif
-            if constexpr (WAVES == 1 && NN <= 42) {
+            if constexpr (WAVES == 1 && NN <= 42 && TGMPC_SWEEP_PAIR) {
+                // One-wave sweep in 2 x 2 pivot blocks (the row-split kernel's block, mpc_split.h): pivots p, p + 1
+                // (p even; n = 2N is even, so no block straddles a padding pivot) are eliminated together,
+                //   a = K_pp, b = K_p+1,p, c = K_p+1,p+1; 1/a; d2 = c - (b/a) b; 1/d2;
+                //   row lanes (u = K_tp, v = K_t,p+1): beta = (v - (u/a) b)/d2, alpha = (u - beta b)/a,
+                //     K_tj <- K_tj - alpha K_pj - beta K_p+1,j, and the block's columns <- (alpha, beta);
+                //   the two RECEIVER lanes (exact zero rows, as in the single form below) take the rows of the block
+                //     inverse G (g00 = 1/a + (b/a)^2/d2, g01 = -(b/a)/d2, g11 = 1/d2) times the pivot rows, and -G.
+                // Both pivot columns are published in one slot as double2 (K_rp, K_r,p+1) under the row r a lane
+                // holds, twice (rotation: the pivot rows in rotated order are the contiguous slice [p, p + NN));
+                // the registers rotate by two per block; receivers are lanes rl(p), rl(p) + 1 with the single form's
+                // rl (NN + p while p < 64 - NN, then the dropped lanes p - (64 - NN), re-zeroed once), so row r
+                // ends in lane (r + NN) mod 64 as there.  The same algebra as two single pivots with one barrier
+                // and one LDS round instead of two; the composed coefficients round differently in the last bits.
+                static_assert(NN % 2 == 0, "pairs of pivots");
+                constexpr int SB2 = 2 * NN;        // double2 per slot (indices rho, rho + NN)
+                static_assert(2 * 2 * SB2 <= NSW, "two slots of double2 columns");
+                constexpr int SPARE = 64 - NN;
+                constexpr int CH = LEAN ? TGMPC_PCH : TGMPC_PAIR_CH;
+                double2* const sw2 = reinterpret_cast<double2*>(__builtin_assume_aligned(s_sw, 16));
+                int rho = t < NN ? t : -1;    // row held by this lane (-1: zero or dropped)
+                if (t < NN) {
+                    const double2 c01 = make_double2(Krow[0], Krow[1]);
+                    sw2[t] = c01;
+                    sw2[t + NN] = c01;
+                }
+                constexpr int SWU = FUSED ? TGMPC_SWEEP_UNROLL : TGMPC_SWEEP_UNROLL_STEP;
+                constexpr int SWU2 = SWU >= 2 ? SWU / 2 : 1;
+#pragma unroll SWU2
+                for (int pv = 0; pv < NN; pv += 2) {
+                    if (NN > SPARE && pv == SPARE) {
+                        // lanes 0..SPARE-1 all pivoted (dropped rows): zero them, they receive next
+                        if (t < SPARE) {
+#pragma unroll
+                            for (int j = 0; j < NN; ++j) Krow[j] = 0.0;
+                        }
+                    }
+                    __syncthreads();
+                    const int o = (pv >> 1) & 1;
+                    // prow[j] = (K_p,p+j, K_p+1,p+j) (rotated; K_r,p = K_p,r)
+                    const double2* prow = sw2 + o * SB2 + pv;
+                    const double2 q0 = prow[0], q1 = prow[1];
+                    double2 cur[CH];
+#pragma unroll
+                    for (int i = 0; i < CH; ++i) if (2 + i < NN) cur[i] = prow[2 + i];
+                    const double a = q0.x, bb = q1.x, cc = q1.y;
+                    const double u = Krow[0], v = Krow[1];
+                    const double ainv = rcp_nr(a);
+                    const double tq = bb * ainv;
+                    const double d2 = fma(-tq, bb, cc);
+                    ok = ok && (a > 0.0) && (d2 > 0.0);
+                    const double d2inv = rcp_nr(d2);
+                    const int rl0 = pv < SPARE ? NN + pv : pv - SPARE;   // receiver lanes rl0, rl0 + 1 (uniform)
+                    const bool r0 = (t == rl0), r1 = (t == rl0 + 1);
+                    const double td = tq * d2inv;
+                    const double beta = fma(-(u * ainv), bb, v) * d2inv;
+                    const double alpha = fma(-beta, bb, u) * ainv;
+                    const double cA = r0 ? fma(td, tq, ainv) : (r1 ? -td : -alpha);
+                    const double cB = r0 ? -td : (r1 ? d2inv : -beta);
+                    rho = r0 ? pv : (r1 ? pv + 1 : ((t == pv || t == pv + 1) ? -1 : rho));
+                    // the next block's columns (registers 2, 3) first, published at once
+                    const double n2 = fma3(cA, cur[0].x, fma(cB, cur[0].y, Krow[2]));
+                    const double n3 = fma3(cA, cur[1].x, fma(cB, cur[1].y, Krow[3]));
+                    if (rho >= 0) {
+                        double2* const nb = sw2 + (o ^ 1) * SB2;
+                        const double2 nn = make_double2(n2, n3);
+                        nb[rho] = nn;
+                        nb[rho + NN] = nn;
+                    }
+                    // Krow[j - 2] <- cA (row p)[j] + cB (row p + 1)[j] + Krow[j], j = 4 .. NN-1, in chunks of CH
+                    // entries, the next chunk's reads issued before this chunk's FMAs
+#pragma unroll
+                    for (int c0 = 2; c0 < NN; c0 += CH) {
+                        double2 nx[CH];
+#pragma unroll
+                        for (int i = 0; i < CH; ++i) if (c0 + CH + i < NN) nx[i] = prow[c0 + CH + i];
+#pragma unroll
+                        for (int i = 0; i < CH; ++i) {
+                            const int j = c0 + i;
+                            if (j >= 4 && j < NN) Krow[j - 2] = fma3(cA, cur[i].x, fma(cB, cur[i].y, Krow[j]));
+                        }
+#pragma unroll
+                        for (int i = 0; i < CH; ++i) cur[i] = nx[i];
+                    }
+                    Krow[0] = n2;
+                    Krow[1] = n3;
+                    Krow[NN - 2] = -cA;
+                    Krow[NN - 1] = -cB;
+                }
+                // row r sits in lane (r + NN) mod 64: rotate it back to lane r
+                const int src = ((t + NN) & 63) << 2;
+#pragma unroll
+                for (int j = 0; j < NN; ++j) {
+                    const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(Krow[j]));
+                    const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(Krow[j]));
+                    Krow[j] = __hiloint2double(hi, lo);
+                    __builtin_amdgcn_sched_barrier(0);   // one register at a time (no batch of 80 temporaries)
+                }
+            } else if constexpr (WAVES == 1 && NN <= 42) {
                 // One-wave sweep, ONE fma per entry and pivot.  The new pivot row (K_pj / d) is not
                 // formed in place (that needs a second operation on the pivot lane only) but in a
                 // RECEIVER lane holding an exact zero row: every lane computes
