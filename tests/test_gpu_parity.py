@@ -666,9 +666,10 @@ def test_dropin_mpc_step_contract(gpu, oracle_lib):
 
 
 @pytest.mark.parametrize("N,Ts,B", [(60, 0.02, 24), (41, 0.05, 16), (60, 0.05, 16), (64, 0.02, 12), (65, 0.02, 8),
-                                    (128, 0.02, 4)])
+                                    (128, 0.02, 4), (21, 0.05, 16), (33, 0.02, 16), (49, 0.05, 12)])
 def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
-    """Horizons past the hot kernels' capacity (TRAJ_MAX_N = 40) run the long-horizon kernel (mpc_long.h: the hot
+    """Horizons past the capacity-40 kernel: 21 <= N <= 64 on the row-split kernel (mpc_split.h; N 21, 41 and 49 open
+    its three half-row widths H = 40 / 48 / 64, N = 33 has n = 66 = 2 mod 4), past that the long-horizon kernel (mpc_long.h: the hot
     algorithm with one thread per variable, K^-1 in LDS up to N = 64, in the caller's scratch from N = 65 to
     TRAJ_MAX_N_LONG = 128; include/trajmpc.h horizon tiers): mpc_step takes any N (mpc_6stati.py:125).  Batch entry
     point and the drop-in module against the oracle at the step tests' bars: statuses identical, iteration counts
