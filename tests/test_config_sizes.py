@@ -67,11 +67,16 @@ def test_configs3_rank_share_through_rccl_gather(gpu, rccl_group, oracle_lib, tm
       the clean rows equal the histories and the noisy rows add each id's own noise draw;
     * the status sidecar's ids and source ids are the generation ids, its worst status the history's;
     * drop_failed=True (opt-in) leaves out exactly the trajectories with a failed step and re-indexes the rest;
-    * along the GPU trajectories of a 64-trajectory sample that includes id 1854, every step re-solved by the
-      step entry point and by the oracle from the GPU's own state agrees: statuses identical; u to 1e-6 where
-      both polished and to 1e-3 where both stopped unpolished at the same ADMM iteration (an eps = 1e-5 ADMM
-      point at a different iteration is a different point: in id 1854's divergent stretch the problem data
-      reach 1e5 and such points differ by 5e-2); polish outcome and iteration counts equal on >= 98 %."""
+    * along the GPU trajectories of ALL 4,096 ids (id 1854 among them), every step re-solved by the step entry
+      point and by the oracle from the GPU's own state agrees: statuses identical; u to 1e-5 where both polished,
+      and to 1e-6 on >= 99.99 % of those; to 2e-4 where both stopped unpolished at the same ADMM iteration (an
+      eps = 1e-5 ADMM point at a different iteration is a different point: in id 1854's divergent stretch the
+      problem data reach 1e5 and such points differ by 5e-2); polish outcome equal on >= 99.9 % and iteration
+      counts on >= 99.99 % of the instance-steps.  The bars against the observed worst (tools/gate_margins.py,
+      profiles/r06_gate_margins.json): 983 k instance-steps, 0 status mismatches, polished |du| <= 2.9e-6 (six
+      ids above 1e-6, all at ordinary steps: borderline active sets that both polishes accept), unpolished
+      same-iteration |du| <= 5.0e-5, polish outcome 99.976 %, iterations 99.9995 %.  (Round 5 sampled 64 ids
+      at 1e-6 / 1e-3 / 98 % / 98 %.)"""
     import pandas as pd
     from trajectory_generation_amd import dataset as D
     from trajectory_generation_amd.workload import make_workload
@@ -134,42 +139,44 @@ def test_configs3_rank_share_through_rccl_gather(gpu, rccl_group, oracle_lib, tm
     np.testing.assert_array_equal(c2["X"].to_numpy().reshape(keep.size, T3 + 1),
                                   Xn[keep, :, 0] + np.stack([D.measurement_noise(i, T3 + 1)[:, 0] for i in keep]))
 
-    # per-step oracle gate along the GPU trajectories of 64 sampled ids (id 1854 among them)
-    rng = np.random.default_rng(3)
-    ids = np.sort(np.concatenate([rng.choice(np.setdiff1d(np.arange(B3), [DIVERGENT_ID]), 63, replace=False),
-                                  [DIVERGENT_ID]]))
-    assert np.array_equal(w["x0"][ids], Xn[ids, 0])
-    vr = np.tile(w["vref"], (ids.size, 1))
+    # per-step oracle gate along the GPU trajectories of every id, 1,024 ids per call
+    ids = np.arange(B3)
+    assert np.array_equal(w["x0"], Xn[:, 0])
+    vr = np.tile(w["vref"], (B3, 1))
     cfg = TB.config_struct(N=N3, Ts=TS3)
     ocfg = oracle_lib.cfg(N=N3, Ts=TS3)
-    n = n_same = n_it = 0
+    n = n_same = n_it = n_both = n_both_tight = 0
     for t in range(T3):
-        xt = Xn[ids, t]
-        ut = Un[ids, t - 1] if t > 0 else w["u0"][ids]
-        fin = np.isfinite(xt).all(axis=1) & np.isfinite(ut).all(axis=1)
-        if not fin.any():
-            break
-        sel = ids[fin]
-        xt, ut = xt[fin], ut[fin]
-        pt = TB.PathSet.build(w["kinds"][sel], w["pcs"][sel], [w["knots"][i] for i in sel])
-        prt = TB.ref_window_batch(pt, xt[:, 0], vr[fin], N3, TS3).cpu().numpy()
-        g = {k: v.cpu().numpy() for k, v in TB.mpc_step_batch(xt, ut, prt, vr[fin], cfg).items()}
-        ro = oracle_lib.mpc_step_batch(xt, ut, prt, vr[fin], ocfg)
-        assert np.array_equal(g["status"], ro["status"]), (t, g["status"], ro["status"])
-        same = (g["polished"] > 0) == (ro["polished"] > 0)
-        ok = g["status"] <= 1
-        du = np.abs(g["u_cmd"] - ro["u_cmd"]).max(axis=1)
-        both = ok & (g["polished"] > 0) & (ro["polished"] > 0)
-        eq = ok & (g["polished"] == 0) & (ro["polished"] == 0) & (g["iters"] == ro["iters"])
-        assert du[both].max(initial=0.0) <= 1e-6, (t, du)
-        assert du[eq].max(initial=0.0) <= 1e-3, (t, du)
-        n_same += int(same.sum())
-        n_it += int((g["iters"] == ro["iters"]).sum())
-        n += int(fin.sum())
+        for c0 in range(0, B3, 1024):
+            sel0 = ids[c0:c0 + 1024]
+            xt = Xn[sel0, t]
+            ut = Un[sel0, t - 1] if t > 0 else w["u0"][sel0]
+            fin = np.isfinite(xt).all(axis=1) & np.isfinite(ut).all(axis=1)
+            if not fin.any():
+                continue
+            sel, xt, ut = sel0[fin], xt[fin], ut[fin]
+            pt = TB.PathSet.build(w["kinds"][sel], w["pcs"][sel], [w["knots"][i] for i in sel])
+            prt = TB.ref_window_batch(pt, xt[:, 0], vr[sel], N3, TS3).cpu().numpy()
+            g = {k: v.cpu().numpy() for k, v in TB.mpc_step_batch(xt, ut, prt, vr[sel], cfg).items()}
+            ro = oracle_lib.mpc_step_batch(xt, ut, prt, vr[sel], ocfg)
+            assert np.array_equal(g["status"], ro["status"]), (t, sel[g["status"] != ro["status"]])
+            same = (g["polished"] > 0) == (ro["polished"] > 0)
+            ok = g["status"] <= 1
+            du = np.abs(g["u_cmd"] - ro["u_cmd"]).max(axis=1)
+            both = ok & (g["polished"] > 0) & (ro["polished"] > 0)
+            eq = ok & (g["polished"] == 0) & (ro["polished"] == 0) & (g["iters"] == ro["iters"])
+            assert du[both].max(initial=0.0) <= 1e-5, (t, sel[both][np.argmax(du[both])], du[both].max())
+            assert du[eq].max(initial=0.0) <= 2e-4, (t, sel[eq][np.argmax(du[eq])], du[eq].max())
+            n_both += int(both.sum())
+            n_both_tight += int((du[both] <= 1e-6).sum())
+            n_same += int(same.sum())
+            n_it += int((g["iters"] == ro["iters"]).sum())
+            n += int(fin.sum())
         if t % 40 == 0:
             print(f"configs[3] per-step gate: step {t}, {n} instance-steps compared", flush=True)
-    assert n >= 0.95 * ids.size * T3
-    assert n_same / n >= 0.98 and n_it / n >= 0.98, (n_same / n, n_it / n)
+    assert n >= 0.95 * B3 * T3
+    assert n_both_tight >= 0.9999 * n_both, (n_both_tight, n_both)
+    assert n_same / n >= 0.999 and n_it / n >= 0.9999, (n_same / n, n_it / n)
 
 
 def test_configs3_whole_job_shards_equal_one_run(gpu):

@@ -342,18 +342,20 @@ def test_closed_loop_per_step_parity_ts005(gpu, oracle_lib, kind, N, T, B, warm)
             assert du[same].max() <= 1e-4
         else:
             # 40-stage problems of the unstable plant reach condition numbers ~1e9:
-            # polished optima agree to 1e-6; unpolished eps = 1e-5 ADMM points to 1e-3 when both stop at
-            # the same iteration (measured <= 1.6e-4); a different stopping iteration is a different point
+            # polished optima agree to 1e-6; unpolished eps = 1e-5 ADMM points to 3e-5 when both stop at
+            # the same iteration; a different stopping iteration is a different point.  Observed on the
+            # row-split kernel (tools/gate_margins.py, profiles/r06_gate_margins.json): 2.5e-7 / 3.0e-6, equal
+            # iterations on 99.7 % (round 5's bars, on the capacity-80 kernel: 1e-6 / 1e-3 / 95 %)
             both = (g["polished"] > 0) & (ro["polished"] > 0)
             assert du[both].max(initial=0.0) <= 1e-6
             eq = same & ~both & (g["iters"] == ro["iters"])
-            assert du[eq].max(initial=0.0) <= 1e-3
+            assert du[eq].max(initial=0.0) <= 3e-5
             n_it += int((g["iters"] == ro["iters"]).sum())
         n_same_pol += same.sum()
         n += B
     assert n_same_pol / n >= 0.98
     if N != 20:
-        assert n_it / n >= 0.95
+        assert n_it / n >= 0.99
 
 
 @pytest.mark.parametrize("kind,N,T,B", [("spline", 20, 20, 48), ("mixed", 40, 20, 32), ("mixed", 48, 12, 16)])
