@@ -5,8 +5,8 @@
 For each gate, every step of the GPU closed loop is re-solved by the step entry point and by the oracle from the
 GPU's own state (as tests/test_config_sizes.py and tests/test_gpu_parity.py do), and the worst observed values of
 the gated quantities are reported instead of asserted:
-  * configs3_all: the configs[3] rank share (4096 spline, N = 20, dt 0.05, 240 steps) over ALL 4096 ids (the test
-    samples 512);
+  * configs3_all: the configs[3] rank share (4096 spline, N = 20, dt 0.05, 240 steps) over all 4096 ids
+    (tests/test_config_sizes.py's gate);
   * n40_ts005: test_closed_loop_per_step_parity_ts005[mixed-40-30-32-0].
 Quantities: status mismatches, max |du| where both polished, max |du| where neither polished at the same ADMM
 iteration (each with the (id, step) where it occurs and the ids above 1e-6), the fractions with equal polish
