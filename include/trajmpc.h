@@ -43,8 +43,9 @@
 extern "C" {
 #endif
 
-#define TRAJMPC_ABI_VERSION 3   /* 2: traj_mpc_qp_batch takes a workspace; traj_mpc_sb_workspace_bytes;
-                                  * 3: the step / QP entry points take horizons up to TRAJ_MAX_N_GENERAL */
+#define TRAJMPC_ABI_VERSION 4   /* 2: traj_mpc_qp_batch takes a workspace; traj_mpc_sb_workspace_bytes;
+                                  * 3: the step / QP entry points take horizons up to TRAJ_MAX_N_GENERAL;
+                                  * 4: the closed loop takes state bounds; traj_closed_loop_workspace_bytes */
 
 /* error codes (return values) */
 #define TRAJ_OK 0
@@ -80,8 +81,8 @@ typedef struct {
     double du_lo[2], du_hi[2];        /* du_bounds :137-138 */
     int has_x_lo, has_x_hi;           /* x_lo / x_hi given (:139-140, :208-213); a side at -inf / inf
                                        * (|bound| >= 1e30) adds no rows.  With a finite bound the step
-                                       * runs the general condensed-QP solver (dense state rows);
-                                       * the closed-loop entry points return TRAJ_E_UNSUPPORTED */
+                                       * runs the general condensed-QP solver (dense state rows), and so
+                                       * does the closed loop (one step per launch sequence, ABI 4) */
     double x_lo[6], x_hi[6];
     double eps_abs, eps_rel, eps_prim_inf, rho, sigma, alpha, delta;
     int max_iter, check_interval, scaling_iters, polish, polish_refine_iter, adaptive_rho;
@@ -109,8 +110,9 @@ typedef struct {
  * Past TRAJ_MAX_N the step and QP entry points take the scratch of traj_mpc_sb_workspace_bytes; the closed-loop entry
  * points (traj_closed_loop_step / _run) run TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG on the long-horizon kernel, one step per
  * launch sequence (rollout, Jacobians, the closed-loop long-horizon solve with the window, warm rho and plant update),
- * with the same extra scratch after the workspace; past TRAJ_MAX_N_LONG, or with state bounds, they return
- * TRAJ_E_UNSUPPORTED (main.py passes no state bounds). */
+ * with the same extra scratch after the workspace; past TRAJ_MAX_N_LONG without state bounds they return
+ * TRAJ_E_UNSUPPORTED.  With state bounds they run the general solver, one step per launch sequence, for every N up to
+ * TRAJ_MAX_N_GENERAL (traj_closed_loop_workspace_bytes sizes the workspace of every case). */
 #define TRAJ_MAX_N 40
 #define TRAJ_MAX_N_SPLIT 64      /* TRAJ_SPLIT_MIN_N <= N <= this: the row-split kernel (mpc_split.h), K^-1 rows in
                                   * registers split across lane pairs */
@@ -193,7 +195,15 @@ typedef struct {
 int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, const double* x_start,
                           const double* vref, double* path_ref, void* stream);
 
-/* One closed-loop step of main.py:85-101 for B trajectories, in place (1 <= N <= TRAJ_MAX_N_LONG, no state bounds):
+/* Workspace bytes of the closed-loop entry points below for configuration c and B trajectories (every tier: the
+ * register-resident and row-split kernels' traj_mpc_workspace_bytes, the long-horizon kernel's scratch after it, and
+ * with state bounds the general solver's scratch plus the step's window and u_cmd); 0 for a configuration the closed
+ * loop does not take. */
+size_t traj_closed_loop_workspace_bytes(const traj_mpc_config* c, int B);
+
+/* One closed-loop step of main.py:85-101 for B trajectories, in place (1 <= N <= TRAJ_MAX_N_LONG; with state bounds
+ * x_lo / x_hi (mpc_6stati.py:208-213) 1 <= N <= TRAJ_MAX_N_GENERAL on the general solver, each step a fresh mpc_step
+ * call -- cold rho, as the reference's per-call loop -- bit-identical to traj_mpc_step_batch on the loop's state):
  *   path_ref = window(x[:,0]); u_cmd = mpc_step(x, u_prev, path_ref, vref); x += Ts f_cont(x, u_cmd);
  *   u_prev = u_cmd.   x [B,6], u_prev [B,2] are updated; vref [B,N+1].
  * If hist_x / hist_u are non-NULL the new state / command are also written to

@@ -81,7 +81,7 @@ def test_struct_layout_matches_c(tmp_path):
 
 
 def test_abi_version_and_strings(L):
-    assert L.traj_abi_version() == 3
+    assert L.traj_abi_version() == 4
     for code, s in _lib.STATUS_STRINGS.items():
         assert L.traj_status_string(code).decode() == s
     for rc in (_lib.TRAJ_OK, _lib.TRAJ_E_ARG, _lib.TRAJ_E_UNSUPPORTED, _lib.TRAJ_E_LAUNCH):
@@ -203,15 +203,27 @@ def test_argument_errors_are_reported_before_any_launch(L):
                                L.traj_mpc_sb_workspace_bytes(4, 20) - 8, nul) == _lib.TRAJ_E_ARG
     ps = _lib.Paths()
     ps.kmax, ps.kind, ps.pc = 0, 16, 16                      # never dereferenced at B = 0
+    # the closed loop takes them too (ABI 4: one step per launch sequence on the general solver), with its scratch
+    # (traj_closed_loop_workspace_bytes: the general solver's plus the step's window and u_cmd) -- a workspace without
+    # it is an argument error before any launch
     assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 0, nul, nul, nul, 0, 0, nul, nul, nul,
-                                   nul, nul, 0, nul) == _lib.TRAJ_E_UNSUPPORTED
+                                   nul, nul, 0, nul) == _lib.TRAJ_OK
+    wcx = L.traj_closed_loop_workspace_bytes(C.byref(cx), 4)
+    assert wcx >= base + L.traj_mpc_sb_workspace_bytes(4, 20) + 4 * (3 * 21 + 2) * 8
+    assert L.traj_closed_loop_workspace_bytes(C.byref(c), 4) == base
+    assert L.traj_closed_loop_step(C.byref(p), C.byref(cx), C.byref(ps), 4, fake, fake, fake, 0, 0, nul, nul, nul,
+                                   nul, fake, wcx - 8, nul) == _lib.TRAJ_E_ARG
+    assert L.traj_closed_loop_run(C.byref(p), C.byref(cx), C.byref(ps), 4, fake, fake, fake, 0, 1, 0, nul, nul, nul,
+                                  nul, fake, wcx - 8, nul) == _lib.TRAJ_E_ARG
     # horizons past the hot kernels' capacity: the closed loop takes them up to TRAJ_MAX_N_LONG (past TRAJ_MAX_N_SPLIT
     # the long-horizon kernel, whose scratch follows the workspace -- a workspace without it is an argument error
-    # before any launch); past that, or with state bounds, it reports them as unsupported, not as an argument error
+    # before any launch); past that without state bounds it reports them as unsupported, not as an argument error
+    # (with state bounds up to TRAJ_MAX_N_GENERAL, the step's own limit; past that an argument error, as for the step)
     cL = _lib.default_config(_lib.MAX_N_SPLIT + 4, 0.05)
     cG = _lib.default_config(_lib.MAX_N_LONG + 1, 0.05)
-    cLx = _lib.default_config(60, 0.05)
+    cLx = _lib.default_config(_lib.MAX_N_GENERAL + 1, 0.05)
     cLx.has_x_lo, cLx.x_lo[3] = 1, -1.0
+    assert L.traj_closed_loop_workspace_bytes(C.byref(cG), 4) == 0 and L.traj_closed_loop_workspace_bytes(C.byref(cLx), 4) == 0
     wsL = L.traj_mpc_workspace_bytes(4, _lib.MAX_N_SPLIT + 4)
     for fn in (L.traj_closed_loop_step, L.traj_closed_loop_run):
         extra = (0, 1) if fn is L.traj_closed_loop_run else (0,)
@@ -219,9 +231,10 @@ def test_argument_errors_are_reported_before_any_launch(L):
                   nul) == _lib.TRAJ_OK
         assert fn(C.byref(p), C.byref(cL), C.byref(ps), 4, fake, fake, fake, *extra, 0, nul, nul, nul, nul, fake, wsL,
                   nul) == _lib.TRAJ_E_ARG
-        for cu in (cG, cLx):
-            assert fn(C.byref(p), C.byref(cu), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
-                      nul) == _lib.TRAJ_E_UNSUPPORTED
+        assert fn(C.byref(p), C.byref(cG), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
+                  nul) == _lib.TRAJ_E_UNSUPPORTED
+        assert fn(C.byref(p), C.byref(cLx), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
+                  nul) == _lib.TRAJ_E_ARG
 
 
 def test_check_raises():

@@ -103,6 +103,7 @@ _SIGS = {
     "traj_lateral_error_batch": (C.c_int, [C.c_int, _V, _V, _V, _V, _V, _V, _V]),
     "traj_mpc_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
     "traj_mpc_sb_workspace_bytes": (C.c_size_t, [C.c_int, C.c_int]),
+    "traj_closed_loop_workspace_bytes": (C.c_size_t, [C.POINTER(MpcConfig), C.c_int]),
     "traj_mpc_step_batch": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.c_int, _V, _V, _V, _V,
                                       _V, _V, _V, _V, _V, _V, _V, _V, C.c_size_t, _V]),
     "traj_mpc_qp_batch": (C.c_int, [C.POINTER(VehicleParams), C.POINTER(MpcConfig), C.c_int, _V, _V, _V, _V, _V,
@@ -178,7 +179,7 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.traj_abi_version() != 3:
+        if L.traj_abi_version() != 4:
             raise RuntimeError("libtrajmpc ABI version mismatch")
         _lib = L
     return _lib

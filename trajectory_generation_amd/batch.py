@@ -334,10 +334,13 @@ def ref_window_batch(paths: PathSet, x_start, vref, N, Ts) -> torch.Tensor:
     return out
 
 
-def _closed_extra(B: int, N: int) -> int:
-    """The closed loop past the register-resident capacity (MAX_N < N <= MAX_N_LONG) runs the long-horizon kernel one
-    step per launch sequence; its scratch follows the workspace (traj_mpc_sb_workspace_bytes), as for the step."""
-    return int(_lib.lib().traj_mpc_sb_workspace_bytes(int(B), int(N))) if N > _lib.MAX_N_SPLIT else 0
+def _closed_extra(B: int, cfg: MpcConfig) -> int:
+    """Bytes the closed loop needs past traj_mpc_workspace_bytes (traj_closed_loop_workspace_bytes): the long-horizon
+    kernel's scratch (MAX_N_SPLIT < N <= MAX_N_LONG), or with state bounds the general solver's plus the step's window
+    and u_cmd (one step per launch sequence, as the step entry point)."""
+    L = _lib.lib()
+    need = int(L.traj_closed_loop_workspace_bytes(C.byref(cfg), int(B)))
+    return max(0, need - int(L.traj_mpc_workspace_bytes(int(B), int(cfg.N))))
 
 
 def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None, t=0, hist_x=None, hist_u=None,
@@ -346,7 +349,7 @@ def closed_loop_step(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=Non
     B = x.shape[0]
     ps = paths.struct()
     T = hist_u.shape[1] if hist_u is not None else 0
-    ws = workspace(B, cfg.N, x.device, _closed_extra(B, cfg.N))
+    ws = workspace(B, cfg.N, x.device, _closed_extra(B, cfg))
     _lib.check(_lib.lib().traj_closed_loop_step(
         C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t), int(T),
         _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()), "traj_closed_loop_step")
@@ -360,7 +363,7 @@ def closed_loop_run(x, u_prev, paths: PathSet, vref, cfg: MpcConfig, params=None
     B = x.shape[0]
     ps = paths.struct()
     T = hist_u.shape[1] if hist_u is not None else 0
-    ws = workspace(B, cfg.N, x.device, _closed_extra(B, cfg.N))
+    ws = workspace(B, cfg.N, x.device, _closed_extra(B, cfg))
     _lib.check(_lib.lib().traj_closed_loop_run(
         C.byref(params_struct(params)), C.byref(cfg), C.byref(ps), B, _p(x), _p(u_prev), _p(vref), int(t0),
         int(steps), int(T), _p(hist_x), _p(hist_u), _p(status), _p(iters), _p(ws), ws.numel() * 8, _stream()),

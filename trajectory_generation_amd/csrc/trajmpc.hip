@@ -115,11 +115,12 @@ __global__ void lateral_error_kernel(int B, const double* X, const double* Y, co
 }
 
 // main.py:51-68 batched (one thread per trajectory: the x-advance is a running sum)
-__global__ void ref_window_kernel(PathArgs pa, int B, int N, double Ts, const double* x_start, const double* vref,
-                                  double* pref) {
+// (xs_stride: x_start[xs_stride b] -- 1 for traj_ref_window_batch, 6 for the closed loop's state rows)
+__global__ void ref_window_kernel(PathArgs pa, int B, int N, double Ts, const double* x_start, int xs_stride,
+                                  const double* vref, double* pref) {
     int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    double xs = x_start[b];
+    double xs = x_start[(size_t)xs_stride * b];
     for (int k = 0; k <= N; ++k) {
         if (k > 0) xs = xs + vref[(size_t)(N + 1) * b + k - 1] * Ts;
         double y, dy;
@@ -637,24 +638,31 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
     if (!x_start || !vref || !path_ref) return TRAJ_E_ARG;
     PathArgs pa{paths->kmax, paths->kind, paths->pc, paths->nk, paths->xk, paths->coef};
     hipLaunchKernelGGL(ref_window_kernel, dim3(nblk(B, 128)), dim3(128), 0, (hipStream_t)stream, pa, B, N, Ts,
-                       x_start, vref, path_ref);
+                       x_start, 1, vref, path_ref);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
 // The closed loop's horizons: N <= TRAJ_MAX_N on the register-resident kernels (fused or per step), TRAJ_MAX_N < N <=
 // TRAJ_MAX_N_LONG on the long-horizon kernel, one step per launch sequence (rollout_kernel + jac_kernel + the closed
-// solve_long_kernel); no state bounds (main.py passes none).  The long tier needs the step's scratch beside the
-// workspace, as the step entry point does: traj_mpc_workspace_bytes + traj_mpc_sb_workspace_bytes.
+// solve_long_kernel).  The long tier needs the step's scratch beside the workspace, as the step entry point does:
+// traj_mpc_workspace_bytes + traj_mpc_sb_workspace_bytes.  With state bounds (mpc_6stati.py:208-213; main.py passes
+// none) any N <= TRAJ_MAX_N_GENERAL, one step per launch sequence on the general solver (closed_step_sb below).
 static int check_cfg_closed(const traj_mpc_config* c) {
-    if (c && ((c->N > TRAJ_MAX_N && c->N <= TRAJ_MAX_N_LONG) || split_route(c))) {
-        const int e = check_cfg(c, true);
-        if (e) return e;
-        return state_bounds_active(c) ? TRAJ_E_UNSUPPORTED : TRAJ_OK;
-    }
+    if (c && ((c->N > TRAJ_MAX_N && c->N <= TRAJ_MAX_N_LONG) || split_route(c) || state_bounds_active(c)))
+        return check_cfg(c, true);
     return check_cfg(c);
+}
+// state bounds: the general solver's scratch after the workspace's base part (as the step's), then the step's window
+// [B, N+1, 3], u_cmd [B, 2] and a status row [B] (int)
+static size_t closed_sb_extra_off(int B, int N) { return ws_base_bytes(B, N) + traj_mpc_sb_workspace_bytes(B, N); }
+static size_t closed_sb_bytes(int B, int N) {
+    const size_t e = closed_sb_extra_off(B, N) + ((size_t)B * (3 * (size_t)(N + 1) + 2) + ((size_t)B + 1) / 2) * sizeof(double);
+    const size_t w = traj_mpc_workspace_bytes(B, N);
+    return e > w ? e : w;
 }
 static size_t closed_ws_bytes(const traj_mpc_config* c, int B) {
     const int N = c->N;   // (the row-split kernel's scratch is in traj_mpc_workspace_bytes; the long-horizon one's follows)
+    if (state_bounds_active(c)) return closed_sb_bytes(B, N);
     return traj_mpc_workspace_bytes(B, N) + ((N > TRAJ_MAX_N && !split_route(c)) ? traj_mpc_sb_workspace_bytes(B, N) : 0);
 }
 // one long-horizon closed-loop step on a's state (a.t = the step, a.status / a.iters = this step's [B] rows)
@@ -669,6 +677,64 @@ static int closed_step_long(const KArgs& a, void* ws, hipStream_t st) {
     stamp(4, st);
     if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
     return e;
+}
+
+// One closed-loop step with state bounds: the step entry point's launches on the loop's own state -- the window
+// (ref_window_kernel on x[:, 0]), the linearization and the general solver (whose u_cmd carries mpc_step's u_prev
+// fallback, mpc_6stati.py:257-262) -- then the plant update and the history (closed_sb_plant_kernel: the closed kernels'
+// tail, main.py:97-101).  Each step is a fresh mpc_step call, as the reference's loop makes it: cold rho, no warm-start
+// record (warm_start has nothing to carry here); the applied u is the step entry point's on the same state, bit for bit.
+__global__ void closed_sb_plant_kernel(const KArgs a, const double* u_cmd) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= a.B) return;
+    double xs[6], f[6], u[2] = {u_cmd[2 * (size_t)b], u_cmd[2 * (size_t)b + 1]};
+    for (int i = 0; i < 6; ++i) xs[i] = a.x_state[6 * (size_t)b + i];
+    f_cont(a.p, xs, u, f);
+    for (int i = 0; i < 6; ++i) {
+        const double xn = xs[i] + a.c.Ts * f[i];
+        a.x_state[6 * (size_t)b + i] = xn;
+        if (a.hist_x) a.hist_x[((size_t)b * (a.hist_T + 1) + a.t + 1) * 6 + i] = xn;
+    }
+    a.u_state[2 * (size_t)b] = u[0];
+    a.u_state[2 * (size_t)b + 1] = u[1];
+    if (a.hist_u) {
+        a.hist_u[((size_t)b * a.hist_T + a.t) * 2] = u[0];
+        a.hist_u[((size_t)b * a.hist_T + a.t) * 2 + 1] = u[1];
+    }
+}
+static int closed_step_sb(const KArgs& a0, void* ws, hipStream_t st) {
+    const int B = a0.B, N = a0.c.N;
+    double* const sws = (double*)((char*)ws + ws_base_bytes(B, N));
+    double* const pr = (double*)((char*)ws + closed_sb_extra_off(B, N));
+    double* const uc = pr + (size_t)B * 3 * (N + 1);
+    int* const sbuf = (int*)(uc + (size_t)B * 2);
+    stamp(0, st);
+    hipLaunchKernelGGL(ref_window_kernel, dim3(nblk(B, 128)), dim3(128), 0, st, a0.path, B, N, a0.c.Ts,
+                       (const double*)a0.x_state, 6, a0.vref, pr);
+    KArgs a = a0;
+    a.x0 = a0.x_state;
+    a.u_prev = a0.u_state;
+    a.path_ref = pr;
+    a.u_cmd = uc;
+    a.status = a0.status ? a0.status : sbuf;
+    a.objective = nullptr; a.X_opt = nullptr; a.U_opt = nullptr; a.polished = nullptr;
+    a.wsWarm = nullptr;
+    a.perm = nullptr;
+    launch_linearize(a, st, false);
+    stamp(1, st);
+    stamp(2, st);
+    stamp(3, st);
+    int e = launch_general(a, sws, st);
+    if (e) return e;
+    hipLaunchKernelGGL(closed_sb_plant_kernel, dim3(nblk(B, 64)), dim3(64), 0, st, a0, (const double*)uc);
+    stamp(4, st);
+    if ((size_t)(5 * g_ev_used + 4) < g_ev.size()) ++g_ev_used;
+    return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
+}
+
+size_t traj_closed_loop_workspace_bytes(const traj_mpc_config* c, int B) {
+    if (!c || B < 0 || check_cfg_closed(c)) return 0;
+    return closed_ws_bytes(c, B);
 }
 
 int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c, const traj_paths* paths, int B,
@@ -700,6 +766,7 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.dbg = g_dbg;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
+    if (state_bounds_active(c)) return closed_step_sb(a, workspace, st);
     if (c->N > TRAJ_MAX_N || split_route(c)) return closed_step_long(a, workspace, st);
     const int nr = (B + 63) / 64, nj = (B * c->N + 63) / 64;
     stamp(0, st);
@@ -764,17 +831,18 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.queue = (int*)(a.wsWarm + (size_t)B * 4) + B;
     if (hipMemsetAsync(a.queue, 0, ((size_t)B * 2 + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
     a.run_ahead = g_run_ahead;
-    if (c->N > TRAJ_MAX_N && !split_route(c)) {
-        // past the row-split capacity: the steps as long-horizon step launch sequences, in order on the stream
-        // (the same results as that many traj_closed_loop_step calls; the queue above stays clear, so
+    if (state_bounds_active(c) || (c->N > TRAJ_MAX_N && !split_route(c))) {
+        // past the row-split capacity, or with state bounds: the steps as step launch sequences, in order on the
+        // stream (the same results as that many traj_closed_loop_step calls; the queue above stays clear, so
         // traj_closed_loop_check reports TRAJ_OK)
+        const bool sb = state_bounds_active(c);
         for (int s = 0; s < steps; ++s) {
             KArgs as = a;
             as.t = t0 + s;
             as.status = status ? status + (size_t)s * B : nullptr;
             as.iters = iters ? iters + (size_t)s * B : nullptr;
             as.nsteps = 0;
-            e = closed_step_long(as, workspace, st);
+            e = sb ? closed_step_sb(as, workspace, st) : closed_step_long(as, workspace, st);
             if (e) return e;
         }
         return TRAJ_OK;
@@ -816,7 +884,7 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
 }
 
 int traj_closed_loop_check(const void* workspace, size_t workspace_bytes, int B, int N, void* stream) {
-    if (B < 0 || N < 1 || N > TRAJ_MAX_N_LONG) return TRAJ_E_ARG;
+    if (B < 0 || N < 1 || N > TRAJ_MAX_N_GENERAL) return TRAJ_E_ARG;
     if (B == 0) return TRAJ_OK;
     if (!workspace || workspace_bytes < traj_mpc_workspace_bytes(B, N)) return TRAJ_E_ARG;
     KArgs a;
