@@ -45,7 +45,8 @@ extern "C" {
 
 #define TRAJMPC_ABI_VERSION 4   /* 2: traj_mpc_qp_batch takes a workspace; traj_mpc_sb_workspace_bytes;
                                   * 3: the step / QP entry points take horizons up to TRAJ_MAX_N_GENERAL;
-                                  * 4: the closed loop takes state bounds; traj_closed_loop_workspace_bytes */
+                                  * 4: the closed loop takes state bounds and every N <= TRAJ_MAX_N_GENERAL (1024);
+                                  *    traj_closed_loop_workspace_bytes */
 
 /* error codes (return values) */
 #define TRAJ_OK 0
@@ -110,15 +111,15 @@ typedef struct {
  * Past TRAJ_MAX_N the step and QP entry points take the scratch of traj_mpc_sb_workspace_bytes; the closed-loop entry
  * points (traj_closed_loop_step / _run) run TRAJ_MAX_N < N <= TRAJ_MAX_N_LONG on the long-horizon kernel, one step per
  * launch sequence (rollout, Jacobians, the closed-loop long-horizon solve with the window, warm rho and plant update),
- * with the same extra scratch after the workspace; past TRAJ_MAX_N_LONG without state bounds they return
- * TRAJ_E_UNSUPPORTED.  With state bounds they run the general solver, one step per launch sequence, for every N up to
- * TRAJ_MAX_N_GENERAL (traj_closed_loop_workspace_bytes sizes the workspace of every case). */
+ * with the same extra scratch after the workspace; with state bounds, or past TRAJ_MAX_N_LONG, they run the general
+ * solver, one step per launch sequence, for every N up to TRAJ_MAX_N_GENERAL (traj_closed_loop_workspace_bytes sizes
+ * the workspace of every case). */
 #define TRAJ_MAX_N 40
 #define TRAJ_MAX_N_SPLIT 64      /* TRAJ_SPLIT_MIN_N <= N <= this: the row-split kernel (mpc_split.h), K^-1 rows in
                                   * registers split across lane pairs */
 #define TRAJ_SPLIT_MIN_N 21
 #define TRAJ_MAX_N_LONG 128
-#define TRAJ_MAX_N_GENERAL 256
+#define TRAJ_MAX_N_GENERAL 1024
 
 int traj_abi_version(void);
 const char* traj_status_string(int status);
@@ -201,9 +202,10 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
  * loop does not take. */
 size_t traj_closed_loop_workspace_bytes(const traj_mpc_config* c, int B);
 
-/* One closed-loop step of main.py:85-101 for B trajectories, in place (1 <= N <= TRAJ_MAX_N_LONG; with state bounds
- * x_lo / x_hi (mpc_6stati.py:208-213) 1 <= N <= TRAJ_MAX_N_GENERAL on the general solver, each step a fresh mpc_step
- * call -- cold rho, as the reference's per-call loop -- bit-identical to traj_mpc_step_batch on the loop's state):
+/* One closed-loop step of main.py:85-101 for B trajectories, in place (1 <= N <= TRAJ_MAX_N_GENERAL; with state
+ * bounds x_lo / x_hi (mpc_6stati.py:208-213), or past TRAJ_MAX_N_LONG, on the general solver, each step a fresh
+ * mpc_step call -- cold rho, as the reference's per-call loop -- bit-identical to traj_mpc_step_batch on the loop's
+ * state):
  *   path_ref = window(x[:,0]); u_cmd = mpc_step(x, u_prev, path_ref, vref); x += Ts f_cont(x, u_cmd);
  *   u_prev = u_cmd.   x [B,6], u_prev [B,2] are updated; vref [B,N+1].
  * If hist_x / hist_u are non-NULL the new state / command are also written to

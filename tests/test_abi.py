@@ -217,13 +217,14 @@ def test_argument_errors_are_reported_before_any_launch(L):
                                   nul, fake, wcx - 8, nul) == _lib.TRAJ_E_ARG
     # horizons past the hot kernels' capacity: the closed loop takes them up to TRAJ_MAX_N_LONG (past TRAJ_MAX_N_SPLIT
     # the long-horizon kernel, whose scratch follows the workspace -- a workspace without it is an argument error
-    # before any launch); past that without state bounds it reports them as unsupported, not as an argument error
-    # (with state bounds up to TRAJ_MAX_N_GENERAL, the step's own limit; past that an argument error, as for the step)
+    # before any launch); past that, and with state bounds, the general solver up to TRAJ_MAX_N_GENERAL (the step's own
+    # limit; past it an argument error, as for the step)
     cL = _lib.default_config(_lib.MAX_N_SPLIT + 4, 0.05)
     cG = _lib.default_config(_lib.MAX_N_LONG + 1, 0.05)
     cLx = _lib.default_config(_lib.MAX_N_GENERAL + 1, 0.05)
     cLx.has_x_lo, cLx.x_lo[3] = 1, -1.0
-    assert L.traj_closed_loop_workspace_bytes(C.byref(cG), 4) == 0 and L.traj_closed_loop_workspace_bytes(C.byref(cLx), 4) == 0
+    assert L.traj_closed_loop_workspace_bytes(C.byref(cLx), 4) == 0
+    assert L.traj_closed_loop_workspace_bytes(C.byref(cG), 4) > L.traj_mpc_sb_workspace_bytes(4, _lib.MAX_N_LONG + 1)
     wsL = L.traj_mpc_workspace_bytes(4, _lib.MAX_N_SPLIT + 4)
     for fn in (L.traj_closed_loop_step, L.traj_closed_loop_run):
         extra = (0, 1) if fn is L.traj_closed_loop_run else (0,)
@@ -232,7 +233,7 @@ def test_argument_errors_are_reported_before_any_launch(L):
         assert fn(C.byref(p), C.byref(cL), C.byref(ps), 4, fake, fake, fake, *extra, 0, nul, nul, nul, nul, fake, wsL,
                   nul) == _lib.TRAJ_E_ARG
         assert fn(C.byref(p), C.byref(cG), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
-                  nul) == _lib.TRAJ_E_UNSUPPORTED
+                  nul) == _lib.TRAJ_OK
         assert fn(C.byref(p), C.byref(cLx), C.byref(ps), 0, nul, nul, nul, *extra, 0, nul, nul, nul, nul, nul, 0,
                   nul) == _lib.TRAJ_E_ARG
 

@@ -761,11 +761,12 @@ def test_step_in_kernel_linearization_bit_identical(gpu, N, Ts):
         assert bool(((a == b) | (torch.isnan(a) & torch.isnan(b))).all()) if a.is_floating_point() else torch.equal(a, b), k
 
 
-@pytest.mark.parametrize("N,B", [(65, 3), (130, 2)])
+@pytest.mark.parametrize("N,B", [(65, 3), (130, 2), (300, 1)])
 def test_general_solver_past_128_variables_vs_oracle(gpu, oracle_lib, N, B):
     """The general solver (state bounds, mpc_general.h) past n = 128 variables, where its one-wave triangular solves
-    hold three or more rows per lane and the Cholesky factor lives in the caller's scratch: statuses, iteration
-    counts and polish outcomes identical to the oracle, U within 1e-6 where both polished (Ts = 0.02, speed band)."""
+    hold three or more rows per lane and the Cholesky factor lives in the caller's scratch -- N = 300 past the round-5
+    limit of 256 (its instance with 32 rows per lane, TRAJ_MAX_N_GENERAL = 1024): statuses, iteration counts and polish
+    outcomes identical to the oracle, U within 1e-6 where both polished (Ts = 0.02, speed band)."""
     x_lo, x_hi = SB["vx"]
     g, r = _sb_both(oracle_lib, 29, B, N, 0.02, 0, x_lo, x_hi)
     assert np.array_equal(g["status"], r["status"])
@@ -895,14 +896,15 @@ def test_state_bound_solves_between_closed_loop_steps(gpu):
 # the closed loop under state bounds: "vcap" caps the speed at 1.3 m/s (the unbounded loop of this workload reaches
 # 1.48 within 40 steps at Ts = 0.05); "wide" as above
 SBC = {"vcap": ([-np.inf, -np.inf, -np.inf, 0.2, -np.inf, -np.inf], [np.inf, np.inf, np.inf, 1.3, np.inf, np.inf]),
-       "wide": SB["wide"]}
+       "wide": SB["wide"], "none": ([-np.inf] * 6, [np.inf] * 6)}
 
 
 @pytest.mark.parametrize("N,Ts,T,B,bounds", [(20, 0.05, 40, 16, "vcap"), (20, 0.02, 30, 16, "wide"),
-                                             (48, 0.02, 8, 6, "vcap")])
+                                             (48, 0.02, 8, 6, "vcap"), (160, 0.02, 3, 2, "none")])
 def test_closed_loop_state_bounds_per_step(gpu, oracle_lib, N, Ts, T, B, bounds):
     """State bounds inside the closed loop (mpc_6stati.py:208-213 passed by main.py:94's call; ABI 4: one step per
-    launch sequence on the general solver, include/trajmpc.h): traj_closed_loop_run equals step-by-step
+    launch sequence on the general solver, include/trajmpc.h), and N = 160 without bounds (past TRAJ_MAX_N_LONG, the
+    same general-solver path): traj_closed_loop_run equals step-by-step
     traj_closed_loop_step calls bit for bit; every step applied exactly the step entry point's u_cmd and status on the
     loop's own state (the reference calls mpc_step once per step: cold rho); and every step re-solved by the oracle
     from the GPU's state agrees at test_state_bounds_vs_oracle's bars (statuses identical, U to 1e-6 where both
@@ -944,6 +946,8 @@ def test_closed_loop_state_bounds_per_step(gpu, oracle_lib, N, Ts, T, B, bounds)
     # on many steps -- the u_prev fallback then holds, as in the reference -- this only checks the bounds leave
     # solvable steps)
     assert (S <= 1).mean() >= 0.15
+    if bounds == "none":   # N = 160, past TRAJ_MAX_N_LONG: the general solver without state rows
+        return
     # the bounds move the loop: the unbounded closed loop of the same workload applies other commands
     un = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts, warm_start=0))
     assert np.abs(un["U"].cpu().numpy() - U).max() > 1e-3

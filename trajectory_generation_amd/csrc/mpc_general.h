@@ -28,7 +28,11 @@ namespace tgmpc {
 
 constexpr int GEN_NT = 256;
 constexpr int GEN_NMAX = 2 * TRAJ_MAX_N;                    // n whose Cholesky factor is kept in LDS
-constexpr int GEN_RMAX = (2 * TRAJ_MAX_N_GENERAL + 63) / 64;  // rows per lane of the one-wave triangular solves
+// rows per lane of the one-wave triangular solves (a register array): the kernel is instantiated for n <= 512 (8 rows
+// per lane, every horizon up to N = 256) and for n <= 2 TRAJ_MAX_N_GENERAL (launch_general picks by n)
+constexpr int GEN_RMAX_SMALL = 8;
+constexpr int GEN_RMAX = (2 * TRAJ_MAX_N_GENERAL + 63) / 64;
+static_assert(GEN_RMAX >= GEN_RMAX_SMALL, "two instances");
 
 // per-instance scratch of solve_gen_kernel, in doubles (m <= 10 N rows; n > GEN_NMAX: + the n x n factor)
 __host__ __device__ inline size_t gen_ws_doubles(int N) {
@@ -172,21 +176,22 @@ __device__ inline bool gen_factor(const GenWs& w, const double* rv, int n, int m
 }
 
 // b <- K^{-1} b with the factor L (chol_solve): wave 0, lane l owns rows l, l + 64, l + 128, ... (GEN_RMAX)
+template <int RMAX>
 __device__ inline void gen_solve(const double* L, int LD, int n, double* b) {
     const int t = threadIdx.x;
     if (t < 64) {
-        double v[GEN_RMAX];
+        double v[RMAX];
 #pragma unroll
-        for (int r = 0; r < GEN_RMAX; ++r) v[r] = (t + 64 * r < n) ? b[t + 64 * r] : 0.0;
+        for (int r = 0; r < RMAX; ++r) v[r] = (t + 64 * r < n) ? b[t + 64 * r] : 0.0;
         for (int k = 0; k < n; ++k) {   // forward: row i's terms in ascending k
             const int owner = k & 63, kr = k >> 6;
             double x = 0.0;
 #pragma unroll
-            for (int r = 0; r < GEN_RMAX; ++r) x = (r == kr) ? v[r] : x;
+            for (int r = 0; r < RMAX; ++r) x = (r == kr) ? v[r] : x;
             if (t == owner) x = x / L[k * LD + k];
             const double bk = __shfl(x, owner);
 #pragma unroll
-            for (int r = 0; r < GEN_RMAX; ++r) {
+            for (int r = 0; r < RMAX; ++r) {
                 const int row = t + 64 * r;
                 if (r == kr && t == owner) v[r] = bk;
                 if (row > k && row < n) v[r] -= L[row * LD + k] * bk;
@@ -196,18 +201,18 @@ __device__ inline void gen_solve(const double* L, int LD, int n, double* b) {
             const int owner = k & 63, kr = k >> 6;
             double x = 0.0;
 #pragma unroll
-            for (int r = 0; r < GEN_RMAX; ++r) x = (r == kr) ? v[r] : x;
+            for (int r = 0; r < RMAX; ++r) x = (r == kr) ? v[r] : x;
             if (t == owner) x = x / L[k * LD + k];
             const double bk = __shfl(x, owner);
 #pragma unroll
-            for (int r = 0; r < GEN_RMAX; ++r) {
+            for (int r = 0; r < RMAX; ++r) {
                 const int row = t + 64 * r;
                 if (r == kr && t == owner) v[r] = bk;
                 if (row < k) v[r] -= L[k * LD + row] * bk;
             }
         }
 #pragma unroll
-        for (int r = 0; r < GEN_RMAX; ++r)
+        for (int r = 0; r < RMAX; ++r)
             if (t + 64 * r < n) b[t + 64 * r] = v[r];
     }
     __syncthreads();
@@ -311,6 +316,7 @@ __device__ inline void gen_active(const GenWs& w, int m, const double* z, const 
 }
 
 // reduced-KKT solve for the active set w.act (kkt_solve_active): x -> w.xpol, y -> w.ypol, A x -> w.Ax
+template <int RMAX>
 __device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, int n, int m, double* L, int LD,
                                       int* s_ok) {
     const int t = threadIdx.x;
@@ -342,7 +348,7 @@ __device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, 
             w.tt[j] = s;
         }
         __syncthreads();
-        gen_solve(L, LD, n, w.tt);
+        gen_solve<RMAX>(L, LD, n, w.tt);
         gen_mv(w.A, m, n, w.tt, w.Ax);
         __syncthreads();
         for (int j = t; j < n; j += GEN_NT) w.xpol[j] += w.tt[j];
@@ -364,6 +370,7 @@ __device__ inline bool gen_kkt_active(const GenWs& w, const traj_mpc_config& c, 
     return true;
 }
 
+template <int RMAX>
 __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double* gws, size_t gstride) {
     __shared__ double s_L[GEN_NMAX * GEN_LD];
     __shared__ double s_red[4 * 14];
@@ -664,7 +671,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                         __syncthreads();
                         for (int j = t; j < n; j += GEN_NT) w.xt[j] = w.rhs[j] + (c.sigma * w.xp[j] - w.q[j]);
                         __syncthreads();
-                        gen_solve(s_Lf, LD, n, w.xt);
+                        gen_solve<RMAX>(s_Lf, LD, n, w.xt);
                         gen_mv(w.A, m, n, w.xt, w.zt);
                         __syncthreads();
                         for (int j = t; j < n; j += GEN_NT) w.x[j] = c.alpha * w.xt[j] + (1.0 - c.alpha) * w.xp[j];
@@ -719,7 +726,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                         int cert = 0, pass;
                         const double tol = c.cert_tol;
                         for (pass = 1; pass <= c.polish_max_pass; ++pass) {
-                            if (!gen_kkt_active(w, c, n, m, s_Lf, LD, &s_i[3])) break;
+                            if (!gen_kkt_active<RMAX>(w, c, n, m, s_Lf, LD, &s_i[3])) break;
                             gen_mv(w.P, n, n, w.xpol, w.Px);
                             gen_mtv(w.A, m, n, w.ypol, w.Aty);
                             __syncthreads();
@@ -772,7 +779,7 @@ __global__ __launch_bounds__(GEN_NT) void solve_gen_kernel(const KArgs a, double
                     } else if (status == TRAJ_STATUS_OPTIMAL && c.polish) {
                         // osqp_polish + OSQP's acceptance rule
                         gen_active(w, m, w.z, w.y);
-                        if (gen_kkt_active(w, c, n, m, s_Lf, LD, &s_i[3])) {
+                        if (gen_kkt_active<RMAX>(w, c, n, m, s_Lf, LD, &s_i[3])) {
                             for (int i = t; i < m; i += GEN_NT) {
                                 const double ztv = w.Ax[i] + w.ypol[i];
                                 const double zz = ztv < w.l[i] ? w.l[i] : (ztv > w.u[i] ? w.u[i] : ztv);

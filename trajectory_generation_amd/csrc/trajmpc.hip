@@ -236,7 +236,10 @@ static int check_cfg(const traj_mpc_config* c, bool allow_sb = false) {
 // the caller's (traj_mpc_sb_workspace_bytes), like every other buffer -- no allocation per call
 static int launch_general(const KArgs& a, double* gws, hipStream_t st) {
     const size_t per = gen_ws_doubles(a.c.N);
-    hipLaunchKernelGGL(solve_gen_kernel, dim3(a.B), dim3(GEN_NT), 0, st, a, gws, per);
+    if (2 * a.c.N <= 64 * GEN_RMAX_SMALL)
+        hipLaunchKernelGGL(solve_gen_kernel<GEN_RMAX_SMALL>, dim3(a.B), dim3(GEN_NT), 0, st, a, gws, per);
+    else
+        hipLaunchKernelGGL(solve_gen_kernel<GEN_RMAX>, dim3(a.B), dim3(GEN_NT), 0, st, a, gws, per);
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
 
@@ -646,10 +649,12 @@ int traj_ref_window_batch(const traj_paths* paths, int B, int N, double Ts, cons
 // TRAJ_MAX_N_LONG on the long-horizon kernel, one step per launch sequence (rollout_kernel + jac_kernel + the closed
 // solve_long_kernel).  The long tier needs the step's scratch beside the workspace, as the step entry point does:
 // traj_mpc_workspace_bytes + traj_mpc_sb_workspace_bytes.  With state bounds (mpc_6stati.py:208-213; main.py passes
-// none) any N <= TRAJ_MAX_N_GENERAL, one step per launch sequence on the general solver (closed_step_sb below).
+// none), or past TRAJ_MAX_N_LONG up to TRAJ_MAX_N_GENERAL, one step per launch sequence on the general solver
+// (closed_step_sb below).
+// (past TRAJ_MAX_N_LONG, or with state bounds: the general solver, closed_step_sb)
+static bool closed_general(const traj_mpc_config* c) { return state_bounds_active(c) || c->N > TRAJ_MAX_N_LONG; }
 static int check_cfg_closed(const traj_mpc_config* c) {
-    if (c && ((c->N > TRAJ_MAX_N && c->N <= TRAJ_MAX_N_LONG) || split_route(c) || state_bounds_active(c)))
-        return check_cfg(c, true);
+    if (c && (c->N > TRAJ_MAX_N || split_route(c) || state_bounds_active(c))) return check_cfg(c, true);
     return check_cfg(c);
 }
 // state bounds: the general solver's scratch after the workspace's base part (as the step's), then the step's window
@@ -662,7 +667,7 @@ static size_t closed_sb_bytes(int B, int N) {
 }
 static size_t closed_ws_bytes(const traj_mpc_config* c, int B) {
     const int N = c->N;   // (the row-split kernel's scratch is in traj_mpc_workspace_bytes; the long-horizon one's follows)
-    if (state_bounds_active(c)) return closed_sb_bytes(B, N);
+    if (closed_general(c)) return closed_sb_bytes(B, N);
     return traj_mpc_workspace_bytes(B, N) + ((N > TRAJ_MAX_N && !split_route(c)) ? traj_mpc_sb_workspace_bytes(B, N) : 0);
 }
 // one long-horizon closed-loop step on a's state (a.t = the step, a.status / a.iters = this step's [B] rows)
@@ -679,7 +684,7 @@ static int closed_step_long(const KArgs& a, void* ws, hipStream_t st) {
     return e;
 }
 
-// One closed-loop step with state bounds: the step entry point's launches on the loop's own state -- the window
+// One closed-loop step on the general solver (state bounds, or N > TRAJ_MAX_N_LONG): the step entry point's launches on the loop's own state -- the window
 // (ref_window_kernel on x[:, 0]), the linearization and the general solver (whose u_cmd carries mpc_step's u_prev
 // fallback, mpc_6stati.py:257-262) -- then the plant update and the history (closed_sb_plant_kernel: the closed kernels'
 // tail, main.py:97-101).  Each step is a fresh mpc_step call, as the reference's loop makes it: cold rho, no warm-start
@@ -766,7 +771,7 @@ int traj_closed_loop_step(const traj_vehicle_params* p, const traj_mpc_config* c
     a.dbg = g_dbg;
     carve_workspace(a, workspace, B, c->N);
     hipStream_t st = (hipStream_t)stream;
-    if (state_bounds_active(c)) return closed_step_sb(a, workspace, st);
+    if (closed_general(c)) return closed_step_sb(a, workspace, st);
     if (c->N > TRAJ_MAX_N || split_route(c)) return closed_step_long(a, workspace, st);
     const int nr = (B + 63) / 64, nj = (B * c->N + 63) / 64;
     stamp(0, st);
@@ -831,11 +836,11 @@ int traj_closed_loop_run(const traj_vehicle_params* p, const traj_mpc_config* c,
     a.queue = (int*)(a.wsWarm + (size_t)B * 4) + B;
     if (hipMemsetAsync(a.queue, 0, ((size_t)B * 2 + 2) * sizeof(int), st) != hipSuccess) return TRAJ_E_LAUNCH;
     a.run_ahead = g_run_ahead;
-    if (state_bounds_active(c) || (c->N > TRAJ_MAX_N && !split_route(c))) {
+    if (closed_general(c) || (c->N > TRAJ_MAX_N && !split_route(c))) {
         // past the row-split capacity, or with state bounds: the steps as step launch sequences, in order on the
         // stream (the same results as that many traj_closed_loop_step calls; the queue above stays clear, so
         // traj_closed_loop_check reports TRAJ_OK)
-        const bool sb = state_bounds_active(c);
+        const bool sb = closed_general(c);
         for (int s = 0; s < steps; ++s) {
             KArgs as = a;
             as.t = t0 + s;
