@@ -45,3 +45,22 @@ def test_struct_cache_keys_signed_zeros_and_types_apart():
     b = _cfg(u_bounds=((-1.0, 1.0), (-0.6, -0.0)))
     assert a is not b
     assert bytes(b) == bytes(TB.config_struct(N=20, Ts=0.05, u_bounds=((-1.0, 1.0), (-0.6, -0.0))))
+
+
+def test_params_key_exact_and_fast_path():
+    """The drop-in's params key (_params_key: names + the values' bits in one pack) separates every changed value,
+    signed zeros included, and leaves non-float values to the generic key (None); the cached params struct is the
+    one params_struct builds."""
+    p = dict(M.Params)
+    k0 = M._params_key(p)
+    assert k0 is not None and k0 == M._params_key(dict(M.Params))
+    for name in p:
+        q = dict(p)
+        q[name] = p[name] * (1.0 + 1e-12) if p[name] != 0.0 else 1e-300
+        assert M._params_key(q) != k0, name
+    z0, z1 = dict(p, vx_zero=0.0), dict(p, vx_zero=-0.0)
+    assert M._params_key(z0) != M._params_key(z1)
+    assert M._params_key(dict(p, m=1)) is None and M._params_key(dict(p, m=np.float64(0.041))) is None
+    s = M._cached_struct("params", lambda: TB.params_struct(p), key=k0)
+    assert s is M._cached_struct("params", lambda: TB.params_struct(p), key=M._params_key(dict(M.Params)))
+    assert bytes(s) == bytes(TB.params_struct(p))

@@ -120,13 +120,27 @@ def _frozen(v):
     return None
 
 
-def _cached_struct(kind, build, *key_parts):
+def _params_key(p: dict):
+    """Exact key of a params dict whose values are all Python floats (the reference's Params and its overrides): the
+    sorted names and the values' bits in one pack -- _frozen's key without its per-item recursion.  None otherwise."""
+    ks = sorted(p)
+    vs = [p[k] for k in ks]
+    if not all(type(v) is float for v in vs):
+        return None
+    return ("pf", tuple(ks), struct.pack("<%dd" % len(vs), *vs))
+
+
+def _cached_struct(kind, build, *key_parts, key=None):
     """config_struct / params_struct for the same arguments as a previous call: the same ctypes struct (the C side
-    copies it at each launch and never writes it).  Arguments without an exact key are built afresh."""
-    parts = tuple(_frozen(k) for k in key_parts)
-    if any(k is None for k in parts):
-        return build()
-    key = (kind,) + parts
+    copies it at each launch and never writes it).  Arguments without an exact key are built afresh.  key: an exact
+    key computed by the caller (replaces the key parts)."""
+    if key is not None:
+        key = (kind, key)
+    else:
+        parts = tuple(_frozen(k) for k in key_parts)
+        if any(k is None for k in parts):
+            return build()
+        key = (kind,) + parts
     v = _STRUCT_CACHE.get(key)
     if v is None:
         if len(_STRUCT_CACHE) > 256:
@@ -259,7 +273,9 @@ def mpc_step(
         "cfg", lambda: _b.config_struct(N=N, Ts=Ts, q_c=q_c, q_phi=q_phi, q_vx=q_vx, R=R, Rd=Rd, u_bounds=u_bounds,
                                         du_bounds=du_bounds, x_lo=x_lo, x_hi=x_hi, **solver_settings),
         N, Ts, q_c, q_phi, q_vx, R, Rd, u_bounds, du_bounds, x_lo, x_hi, tuple(sorted(solver_settings.items())))
-    pst = _cached_struct("params", lambda: _b.params_struct(p), tuple(sorted(p.items())))
+    pk = _params_key(p)
+    pst = (_cached_struct("params", lambda: _b.params_struct(p), key=pk) if pk is not None
+           else _cached_struct("params", lambda: _b.params_struct(p), tuple(sorted(p.items()))))
     # one staged copy in: [x0 6 | u_prev 2 | path_ref 3(N+1) | vref N+1]; one copy out:
     # [u_cmd 2 | objective 1 | X_opt 6(N+1) | U_opt 2N | status, iters, polished (int32)]
     dev = _b.require_gpu()
