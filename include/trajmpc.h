@@ -103,8 +103,8 @@ typedef struct {
  *                                        each row split across a lane pair joined by v_permlane32_swap, 2 waves per
  *                                        SIMD; the QP entry point keeps the two-wave capacity-80 kernel up to TRAJ_MAX_N);
  *   TRAJ_MAX_N_SPLIT < N <= TRAJ_MAX_N_LONG  without state bounds: the long-horizon kernel (mpc_long.h: the hot kernels'
- *                                        algorithm with one thread per QP variable, K^-1 in LDS up to N = 64 and in
- *                                        the caller's scratch beyond);
+ *                                        algorithm with one thread per QP variable -- 256 threads, 512 past N = 128 --
+ *                                        K^-1 in LDS up to N = 64 and in the caller's scratch beyond);
  *   otherwise (state bounds, or N > TRAJ_MAX_N_LONG up to TRAJ_MAX_N_GENERAL) the general condensed-QP solver
  *                                        (mpc_general.h, one 256-thread workgroup per instance, its Cholesky factor
  *                                        in the caller's scratch).
@@ -118,7 +118,7 @@ typedef struct {
 #define TRAJ_MAX_N_SPLIT 64      /* TRAJ_SPLIT_MIN_N <= N <= this: the row-split kernel (mpc_split.h), K^-1 rows in
                                   * registers split across lane pairs */
 #define TRAJ_SPLIT_MIN_N 21
-#define TRAJ_MAX_N_LONG 128
+#define TRAJ_MAX_N_LONG 256   /* 128 < N: the long-horizon kernel's 512-thread instance (round 6) */
 #define TRAJ_MAX_N_GENERAL 1024
 
 int traj_abi_version(void);

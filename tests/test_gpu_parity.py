@@ -668,12 +668,12 @@ def test_dropin_mpc_step_contract(gpu, oracle_lib):
 
 
 @pytest.mark.parametrize("N,Ts,B", [(60, 0.02, 24), (41, 0.05, 16), (60, 0.05, 16), (64, 0.02, 12), (65, 0.02, 8),
-                                    (128, 0.02, 4), (21, 0.05, 16), (33, 0.02, 16), (49, 0.05, 12)])
+                                    (128, 0.02, 4), (21, 0.05, 16), (33, 0.02, 16), (49, 0.05, 12), (200, 0.02, 4)])
 def test_long_horizon_vs_oracle(gpu, oracle_lib, N, Ts, B):
     """Horizons past the capacity-40 kernel: 21 <= N <= 64 on the row-split kernel (mpc_split.h; N 21, 41 and 49 open
     its three half-row widths H = 40 / 48 / 64, N = 33 has n = 66 = 2 mod 4), past that the long-horizon kernel (mpc_long.h: the hot
     algorithm with one thread per variable, K^-1 in LDS up to N = 64, in the caller's scratch from N = 65 to
-    TRAJ_MAX_N_LONG = 128; include/trajmpc.h horizon tiers): mpc_step takes any N (mpc_6stati.py:125).  Batch entry
+    TRAJ_MAX_N_LONG = 256, N > 128 on its 512-thread instance; include/trajmpc.h horizon tiers): mpc_step takes any N (mpc_6stati.py:125).  Batch entry
     point and the drop-in module against the oracle at the step tests' bars: statuses identical, iteration counts
     equal on >= 95 %, U within 1e-6 where both polished and 1e-4 where neither did; the drop-in returns the batch's
     u_cmd and the reference's fallback contract."""
@@ -900,11 +900,13 @@ SBC = {"vcap": ([-np.inf, -np.inf, -np.inf, 0.2, -np.inf, -np.inf], [np.inf, np.
 
 
 @pytest.mark.parametrize("N,Ts,T,B,bounds", [(20, 0.05, 40, 16, "vcap"), (20, 0.02, 30, 16, "wide"),
-                                             (48, 0.02, 8, 6, "vcap"), (160, 0.02, 3, 2, "none")])
+                                             (48, 0.02, 8, 6, "vcap"), (160, 0.02, 3, 2, "none"),
+                                             (300, 0.02, 2, 2, "none")])
 def test_closed_loop_state_bounds_per_step(gpu, oracle_lib, N, Ts, T, B, bounds):
     """State bounds inside the closed loop (mpc_6stati.py:208-213 passed by main.py:94's call; ABI 4: one step per
-    launch sequence on the general solver, include/trajmpc.h), and N = 160 without bounds (past TRAJ_MAX_N_LONG, the
-    same general-solver path): traj_closed_loop_run equals step-by-step
+    launch sequence on the general solver, include/trajmpc.h), and without bounds N = 160 (the long-horizon kernel's
+    512-thread instance) and N = 300 (past TRAJ_MAX_N_LONG: the general-solver path): traj_closed_loop_run equals
+    step-by-step
     traj_closed_loop_step calls bit for bit; every step applied exactly the step entry point's u_cmd and status on the
     loop's own state (the reference calls mpc_step once per step: cold rho); and every step re-solved by the oracle
     from the GPU's state agrees at test_state_bounds_vs_oracle's bars (statuses identical, U to 1e-6 where both
@@ -914,7 +916,9 @@ def test_closed_loop_state_bounds_per_step(gpu, oracle_lib, N, Ts, T, B, bounds)
     x_lo, x_hi = SBC[bounds]
     w = make_workload(B, N, Ts, kind="spline", seed=5)
     paths = TB.PathSet.build(w["kinds"], w["pcs"], w["knots"])
-    cfg = TB.config_struct(N=N, Ts=Ts, x_lo=x_lo, x_hi=x_hi)
+    # (cold rho, the reference's per-call semantics: the bounded and the general-solver closed loop run it anyway; the
+    # long-horizon kernel's closed loop (N = 160) would otherwise carry rho from step to step)
+    cfg = TB.config_struct(N=N, Ts=Ts, x_lo=x_lo, x_hi=x_hi, warm_start=0)
     res = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg)
     ref = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, cfg, fused=False)
     for k in ("X", "U", "status", "iters"):
@@ -942,12 +946,12 @@ def test_closed_loop_state_bounds_per_step(gpu, oracle_lib, N, Ts, T, B, bounds)
         n_pol += int((pg == pr).sum())
         n_it += int((g["iters"] == ro["iters"]).sum())
     assert n_pol / n >= 0.95 and n_it / n >= 0.95, (n_pol / n, n_it / n)
+    if bounds == "none":   # (no state rows: nothing below applies)
+        return
     # (the statuses are the oracle's, step by step; with state rows OSQP stops unconverged or certifies infeasibility
     # on many steps -- the u_prev fallback then holds, as in the reference -- this only checks the bounds leave
     # solvable steps)
     assert (S <= 1).mean() >= 0.15
-    if bounds == "none":   # N = 160, past TRAJ_MAX_N_LONG: the general solver without state rows
-        return
     # the bounds move the loop: the unbounded closed loop of the same workload applies other commands
     un = TB.run_closed_loop(w["x0"], w["u0"], paths, w["vref"], T, TB.config_struct(N=N, Ts=Ts, warm_start=0))
     assert np.abs(un["U"].cpu().numpy() - U).max() > 1e-3

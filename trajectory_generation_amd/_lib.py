@@ -20,7 +20,7 @@ TRAJ_OK, TRAJ_E_ARG, TRAJ_E_UNSUPPORTED, TRAJ_E_LAUNCH, TRAJ_E_HANDOFF = 0, -1, 
 MAX_N = 40            # hot kernels, every entry point (include/trajmpc.h TRAJ_MAX_N)
 MAX_N_SPLIT = 64      # the row-split kernel for SPLIT_MIN_N <= N <= MAX_N_SPLIT (TRAJ_MAX_N_SPLIT)
 SPLIT_MIN_N = 21      # TRAJ_SPLIT_MIN_N
-MAX_N_LONG = 128      # step / QP entry points on the long-horizon kernel without state bounds (TRAJ_MAX_N_LONG)
+MAX_N_LONG = 256      # step / QP entry points on the long-horizon kernel without state bounds (TRAJ_MAX_N_LONG)
 MAX_N_GENERAL = 1024  # step / QP entry points on the general solver (TRAJ_MAX_N_GENERAL)
 
 STATUS_STRINGS = {

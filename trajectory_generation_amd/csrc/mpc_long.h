@@ -14,7 +14,7 @@
 // u_prev from the closed-loop buffers, the reference window from the state (main.py:51-68, as mpc_solve.h does), the
 // warm-start rho carried in the workspace's warm record, and the plant update x <- x + Ts f(x, u_cmd) (:97), u_prev
 // <- u_cmd (:101) with the history, instead of X_opt / U_opt / the objective.
-// Layout: one 256-thread workgroup per instance, thread t owns variable t (n <= 256).  The scaled P lives in the
+// Layout: one NT-thread workgroup per instance (NT = 256, or 512 past n = 256), thread t owns variable t (n <= NT).  The scaled P lives in the
 // caller's scratch, COLUMN-major (entry (r, j) at j ld + r: for fixed j the threads read consecutive doubles), ld x ld
 // with ld = n rounded up to 8 and zero padding; K^-1 the same way, in LDS (dynamic shared memory, n <= LONG_NKL:
 // 128 KB at n = 128) or in the scratch beyond.  A pivot of the sweep, a mat-vec, a Ruiz pass each stream the
@@ -27,7 +27,8 @@
 
 namespace tgmpc {
 
-constexpr int LONG_NT = 256;                  // threads per instance = max n
+constexpr int LONG_NT = 256;                  // threads per instance = max n (n <= 256)
+constexpr int LONG_NT2 = 512;                 // the instance for 256 < n <= 512 (round 6: N up to 256)
 constexpr int LONG_NKL = 128;                 // n up to which K^-1 lives in LDS
 
 __host__ __device__ inline int long_ld(int n) { return (n + 7) & ~7; }
@@ -41,19 +42,19 @@ __host__ inline size_t long_lds_bytes(int N) {
     return n <= LONG_NKL ? (size_t)long_ld(n) * long_ld(n) * sizeof(double) : 0;
 }
 
-template <bool KL, bool CLOSED = false>
-__global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, double* lws, size_t lstride) {
+template <bool KL, bool CLOSED = false, int NT = LONG_NT>
+__global__ __launch_bounds__(NT) void solve_long_kernel(const KArgs a, double* lws, size_t lstride) {
     extern __shared__ __attribute__((aligned(16))) double s_kl[];   // K^-1 (KL)
-    __shared__ double s_bc[2][LONG_NT];       // broadcast vectors (rotating)
-    __shared__ double s_ex[4][LONG_NT];       // +-2 exchanges (rotating)
-    __shared__ double s_pc[LONG_NT];          // the sweep's pivot column
+    __shared__ double s_bc[2][NT];       // broadcast vectors (rotating)
+    __shared__ double s_ex[4][NT];       // +-2 exchanges (rotating)
+    __shared__ double s_pc[NT];          // the sweep's pivot column
     __shared__ double s_xh[6];                // free response, one stage
-    __shared__ double s_F[3][LONG_NT];        // condensing: F_k rows
-    __shared__ double s_red[4 * 8];
+    __shared__ double s_F[3][NT];        // condensing: F_k rows
+    __shared__ double s_red[(NT / 64) * 8];
     __shared__ int s_flag[4];
     // CLOSED: the step's state, u_prev and reference window (main.py:51-68) -- x_state / u_state are overwritten by the
     // plant update at the end, so every read goes through these copies
-    __shared__ double s_xc[CLOSED ? 6 : 1], s_uc[CLOSED ? 2 : 1], s_prc[CLOSED ? 3 * (LONG_NT / 2 + 1) : 1];
+    __shared__ double s_xc[CLOSED ? 6 : 1], s_uc[CLOSED ? 2 : 1], s_prc[CLOSED ? 3 * (NT / 2 + 1) : 1];
     const int b = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
     const traj_vehicle_params& p = a.p;
     const traj_mpc_config& c = a.c;
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
             }
         }
         __syncthreads();
-        for (int k = t; k <= N; k += LONG_NT) {
+        for (int k = t; k <= N; k += NT) {
             double y, dy;
             path_eval(a.path, b, s_prc[3 * k], y, dy);
             s_prc[3 * k + 1] = y;
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             double m = s_red[i];
-            for (int w = 1; w < LONG_NT / 64; ++w) m = fmax(m, s_red[w * 8 + i]);
+            for (int w = 1; w < NT / 64; ++w) m = fmax(m, s_red[w * 8 + i]);
             v[i] = nan[i] ? __builtin_nan("") : m;
         }
         __syncthreads();
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         if (lane == 0) s_red[wid * 8] = v;
         __syncthreads();
         double s = 0.0;
-        for (int w = 0; w < LONG_NT / 64; ++w) s += s_red[w * 8];
+        for (int w = 0; w < NT / 64; ++w) s += s_red[w * 8];
         __syncthreads();
         return s;
     };
@@ -194,8 +195,8 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         int bad = 0;
         if (t < 6) bad |= !isfinite(x0[t]);
         if (t < 2) bad |= !isfinite(up[t]);
-        for (int i = t; i < 3 * (N + 1); i += LONG_NT) bad |= !isfinite(pref[i]);
-        for (int i = t; i < N + 1; i += LONG_NT) bad |= !isfinite(vr[i]);
+        for (int i = t; i < 3 * (N + 1); i += NT) bad |= !isfinite(pref[i]);
+        for (int i = t; i < N + 1; i += NT) bad |= !isfinite(vr[i]);
         if (bad) s_flag[0] = 1;
     }
 
@@ -658,7 +659,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         }
         return;
     }
-    // X_{k+1} = A_k X_k + B_k U_k + g_k, stage by stage (thread r < 6: state r); X in s_ex (6 (N+1) <= 4 * 256)
+    // X_{k+1} = A_k X_k + B_k U_k + g_k, stage by stage (thread r < 6: state r); X in s_ex (6 (N+1) <= 4 NT)
     double* const Xs = &s_ex[0][0];
     if (t < 6) Xs[t] = x0[t];
     __syncthreads();
@@ -672,7 +673,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
         __syncthreads();
     }
     double op = 0.0;
-    for (int k = t; k <= N; k += LONG_NT) {
+    for (int k = t; k <= N; k += NT) {
         const double* X = Xs + 6 * k;
         double s, co;
         pm_sincos(pref[3 * k + 2], &s, &co);
@@ -699,7 +700,7 @@ __global__ __launch_bounds__(LONG_NT) void solve_long_kernel(const KArgs a, doub
     }
     if (a.U_opt && own) a.U_opt[(size_t)b * 2 * N + ch * N + kk] = good ? xsol : nan;
     if (a.X_opt)
-        for (int i = t; i < 6 * (N + 1); i += LONG_NT) {
+        for (int i = t; i < 6 * (N + 1); i += NT) {
             const int rr = i / (N + 1), k = i % (N + 1);
             a.X_opt[(size_t)b * 6 * (N + 1) + i] = good ? Xs[6 * k + rr] : nan;
         }

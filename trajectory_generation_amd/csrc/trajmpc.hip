@@ -265,8 +265,10 @@ static int launch_long(const KArgs& a, double* lws, hipStream_t st) {
             if (dev >= 0 && dev < 64) attr[dev].store(true, std::memory_order_release);
         }
         hipLaunchKernelGGL((solve_long_kernel<true, CLOSED>), dim3(a.B), dim3(LONG_NT), lds, st, a, lws, per);
-    } else {
+    } else if (2 * N <= LONG_NT) {
         hipLaunchKernelGGL((solve_long_kernel<false, CLOSED>), dim3(a.B), dim3(LONG_NT), 0, st, a, lws, per);
+    } else {   // 128 < N <= TRAJ_MAX_N_LONG: the 512-thread instance (round 6)
+        hipLaunchKernelGGL((solve_long_kernel<false, CLOSED, LONG_NT2>), dim3(a.B), dim3(LONG_NT2), 0, st, a, lws, per);
     }
     return hipGetLastError() == hipSuccess ? TRAJ_OK : TRAJ_E_LAUNCH;
 }
